@@ -1,0 +1,71 @@
+"""ctypes binding of libast_hip.so (the C ABI declared in include/ast_hip.h).
+
+The library is built in-tree (`python -c "import __graft_entry__ as g; g.build()"`). There is no
+fallback: if the library is missing, or a tensor is not on a HIP device, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads PyTorch's HIP runtime first, so the library binds to the same one)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libast_hip.so")
+
+_c_float_p = ctypes.c_void_p
+_i = ctypes.c_int
+_ll = ctypes.c_longlong
+_p = ctypes.c_void_p
+
+# name -> (restype, argtypes); must match include/ast_hip.h exactly (tests/test_capi.py checks it)
+SIGNATURES = {
+    "ast_version": (ctypes.c_char_p, []),
+    "ast_conv3x3_packed_numel": (ctypes.c_size_t, [_i, _i]),
+    "ast_conv3x3_pack_weights_f32": (_i, [_p, _p, _i, _i, _p]),
+    "ast_conv3x3_fwd_f32": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "ast_conv3x3_num_configs": (_i, []),
+    "ast_conv3x3_fwd_f32_cfg": (_i, [_i, _p, _p, _i, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "ast_channel_stats_f32": (_i, [_p, _p, _p, _ll, _ll, _i, ctypes.c_float, _p]),
+    "ast_adain_f32": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, ctypes.c_double, _i, _p]),
+    "ast_plane_normalize_f32": (_i, [_p, _p, _p, _p, _ll, _ll, _p]),
+}
+
+ERRORS = {-1: "null pointer", -2: "bad shape", -3: "unsupported configuration"}
+
+_lib = None
+
+
+class HipOpError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raises if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipOpError(
+                f"{LIB_PATH} is missing: build the HIP extension first "
+                "(python -c 'import __graft_entry__ as g; g.build()'). There is no CPU fallback.")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        msg = ERRORS.get(code, f"hipError_t {code}")
+        raise HipOpError(f"{what} failed: {msg}")
+
+
+def stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()

@@ -1,0 +1,472 @@
+// 3x3 stride-1 convolution as an MFMA-fp32 implicit GEMM for gfx950 (MI355X / CDNA4).
+//
+// Replaces the reference's nn.Conv2d(k3,p1)+ReLU(+MaxPool) chain of PretrainedEncoder
+// (models.py:199-240) and the [Upsample]+ReflectionPad+Conv+ReLU chain of the mirrored decoder
+// (models.py:598-628). GEMM view: out[pixel][cout] = sum_{cin,tap} in[pixel+tap][cin] * w[cin,tap][cout].
+//
+// Design:
+//  * v_mfma_f32_32x32x2_f32: exact fp32 products (an fmaf chain), 64 FLOP/clk/SIMD = the
+//    157.3 TF fp32 matrix peak. Lane l feeds A[i=l&31][k=l>>5] and B[k=l>>5][j=l&31].
+//  * M = one 32-pixel output row segment per MFMA tile (lanes -> consecutive x: conflict-free
+//    LDS reads and float4 NCHW stores), N = 32 output channels, K pair = two input channels at
+//    the same tap.
+//  * A workgroup owns a TH x 32 output tile x BN channels. Per K-chunk of CK input channels it
+//    stages the SOURCE tile (before the x2 nearest upsample) with a 1-pixel halo in LDS: float4
+//    row loads for the interior, scalar loads for the two halo columns, rows remapped for
+//    zero / reflect padding. Upsample + reflect padding of the upsampled grid equals
+//    replicate-padding of the source grid, so both are resolved by the per-lane LDS read
+//    address. The conv_1 ImageNet normalisation is applied to loaded values (padding stays 0,
+//    as the reference pads the normalised image). The CK x 9 x BN weight slab is staged beside
+//    it; both double-buffered, next chunk's global loads in flight while the MFMAs run.
+//  * Epilogue: bias, optional pre-ReLU store (the conv_i taps of the loss network), ReLU store,
+//    and a fused 2x2 max-pool done in registers (a lane holds both rows of a window).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/ast_hip.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int TW = 32;  // output tile width = one MFMA M-tile
+
+struct ConvArgs {
+  const float* x;
+  const float* x2;  // optional second input batch: images [nsplit, N) read from x2 (content|style pair)
+  int nsplit;
+  const float* wp;  // packed [cin_pad][9][cout_pad]
+  const float* bias;
+  float* y_pre;
+  float* y_act;
+  float* y_pool;
+  const float* in_mean;
+  const float* in_std;
+  int N, Cin, Hin, Win, Cout, H, W;
+  int cin_pad, cout_pad;
+  int reflect;  // 0: zero pad, 1: reflect pad (of the upsampled grid)
+  int tiles_x, tiles_y;
+};
+
+constexpr int kCinAlign = 8;    // packed cin padding (>= every CK)
+constexpr int kCoutAlign = 64;  // packed cout padding
+
+// Source-grid index of padded coordinate g (may be -1 or n) for the pad mode; -1 = zero.
+//  reflect, no upsample: ReflectionPad2d(1)        -> reflect
+//  reflect, upsample x2: reflect on 2n grid        -> replicate on the n grid
+//  zeros:                                          -> -1 outside
+template <int UP>
+__device__ __forceinline__ int src_index(int g, int n, int reflect) {
+  if (g >= 0 && g < n) return g;
+  if (!reflect) return -1;
+  if (UP == 2) return g < 0 ? 0 : n - 1;
+  int r = g < 0 ? -g : 2 * (n - 1) - g;
+  return r < 0 ? 0 : (r >= n ? n - 1 : r);
+}
+
+// torch semantics: relu(NaN) = NaN, max_pool propagates NaN.
+__device__ __forceinline__ float relu_f(float v) { return v < 0.f ? 0.f : v; }
+__device__ __forceinline__ float max_nan(float a, float b) { return (b > a || b != b) ? b : a; }
+
+template <int WM, int WN, int RM, int RN, int CK, int UP>
+struct Cfg {
+  static constexpr int NT = WM * WN * 64;
+  static constexpr int TH = WM * RM;             // output rows per tile
+  static constexpr int BN = WN * RN * 32;        // output channels per tile
+  static constexpr int SW = TW / UP;             // source columns per tile (interior)
+  static constexpr int SR = TH / UP + 2;         // source rows per tile incl. halo
+  static constexpr int RS = SW + 8;              // LDS row stride: [pad3|halo|interior(16B aligned)|halo|pad]
+  static constexpr int C0 = 4;                   // LDS column of source column sx0
+  static constexpr int A_ELEMS = CK * SR * RS;
+  static constexpr int B_ELEMS = CK * 9 * BN;
+  static constexpr int QV = SW / 4;              // float4 per interior row
+  static constexpr int A_ITEMS = CK * SR * (QV + 2);     // fast path: QV vectors + 2 halo scalars per row
+  static constexpr int A_PER_T = (A_ITEMS + NT - 1) / NT;
+  static constexpr int S_ITEMS = CK * SR * (SW + 2);     // slow path: scalar per column
+  static constexpr int B_VEC = B_ELEMS / 4;
+  static constexpr int B_PER_T = (B_VEC + NT - 1) / NT;
+  static constexpr int LDS_BYTES = 2 * (A_ELEMS + B_ELEMS) * 4;
+};
+
+template <int WM, int WN, int RM, int RN, int CK, int UP>
+__global__ __launch_bounds__(WM * WN * 64, 2) void conv3x3_f32_kernel(ConvArgs a) {
+  using C = Cfg<WM, WN, RM, RN, CK, UP>;
+  constexpr int NT = C::NT, TH = C::TH, BN = C::BN, SW = C::SW, SR = C::SR, RS = C::RS, QV = C::QV;
+  constexpr int A_ELEMS = C::A_ELEMS, B_ELEMS = C::B_ELEMS;
+  static_assert(CK % 2 == 0, "two channels per MFMA k-pair");
+  static_assert(TH % 2 == 0, "even tile height (pool windows, upsample row pairs)");
+  static_assert(UP == 1 || UP == 2, "");
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* As = smem;                // [2][CK][SR][RS]
+  float* Bs = smem + 2 * A_ELEMS;  // [2][CK*9][BN]
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int wm = wave % WM, wn = wave / WM;
+
+  int t = blockIdx.x;
+  const int tx = t % a.tiles_x;
+  t /= a.tiles_x;
+  const int ty = t % a.tiles_y;
+  const int n = t / a.tiles_y;
+  const int x0 = tx * TW, y0 = ty * TH;
+  const int sx0 = x0 / UP, sy0 = y0 / UP - 1;  // source tile origin (row includes the halo)
+  const int n0 = blockIdx.y * BN;
+  const int Hin = a.Hin, Win = a.Win;
+  const bool fast = (sx0 + SW <= Win) && ((Win & 3) == 0);  // block-uniform
+
+  const float* __restrict__ xin =
+      n < a.nsplit ? a.x + (int64_t)n * a.Cin * Hin * Win : a.x2 + (int64_t)(n - a.nsplit) * a.Cin * Hin * Win;
+  const int plane_in = Hin * Win;
+
+  float4 ra[C::A_PER_T];
+  float4 rb[C::B_PER_T];
+
+  // ---- global -> registers (chunk starting at input channel cin0) ----
+  auto load_a_fast = [&](int cin0) {
+#pragma unroll
+    for (int i = 0; i < C::A_PER_T; ++i) {
+      const int e = tid + i * NT;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < C::A_ITEMS) {
+        const int q = e % (QV + 2);
+        const int cr = e / (QV + 2);
+        const int r = cr % SR, c = cr / SR;
+        const int cin = cin0 + c;
+        const int sy = src_index<UP>(sy0 + r, Hin, a.reflect);
+        if (cin < a.Cin && sy >= 0) {
+          const float* row = xin + cin * plane_in + sy * Win;
+          if (q < QV) {
+            v = *reinterpret_cast<const float4*>(row + sx0 + 4 * q);
+            if (a.in_mean) {
+              const float m = a.in_mean[cin], s = a.in_std[cin];
+              v.x = (v.x - m) / s; v.y = (v.y - m) / s; v.z = (v.z - m) / s; v.w = (v.w - m) / s;
+            }
+          } else {
+            const int sx = src_index<UP>(q == QV ? sx0 - 1 : sx0 + SW, Win, a.reflect);
+            if (sx >= 0) {
+              v.x = row[sx];
+              if (a.in_mean) v.x = (v.x - a.in_mean[cin]) / a.in_std[cin];
+            }
+          }
+        }
+      }
+      ra[i] = v;
+    }
+  };
+  auto store_a_fast = [&](float* as) {
+#pragma unroll
+    for (int i = 0; i < C::A_PER_T; ++i) {
+      const int e = tid + i * NT;
+      if (e < C::A_ITEMS) {
+        const int q = e % (QV + 2);
+        const int cr = e / (QV + 2);
+        float* row = as + cr * RS;
+        if (q < QV) *reinterpret_cast<float4*>(row + C::C0 + 4 * q) = ra[i];
+        else row[q == QV ? C::C0 - 1 : C::C0 + SW] = ra[i].x;
+      }
+    }
+  };
+  // Irregular tiles (right edge narrower than the tile, or W % 4 != 0): scalar gather into LDS.
+  auto fill_a_slow = [&](int cin0, float* as) {
+    for (int e = tid; e < C::S_ITEMS; e += NT) {
+      const int col = e % (SW + 2);
+      const int cr = e / (SW + 2);
+      const int r = cr % SR, c = cr / SR;
+      const int cin = cin0 + c;
+      const int sy = src_index<UP>(sy0 + r, Hin, a.reflect);
+      const int sx = src_index<UP>(sx0 - 1 + col, Win, a.reflect);
+      float v = 0.f;
+      if (cin < a.Cin && sy >= 0 && sx >= 0) {
+        v = xin[cin * plane_in + sy * Win + sx];
+        if (a.in_mean) v = (v - a.in_mean[cin]) / a.in_std[cin];
+      }
+      as[cr * RS + C::C0 - 1 + col] = v;
+    }
+  };
+  auto load_b = [&](int cin0) {
+#pragma unroll
+    for (int i = 0; i < C::B_PER_T; ++i) {
+      const int vi = tid + i * NT;
+      if (vi < C::B_VEC) {
+        const int f = vi * 4;
+        const int row = f / BN;  // = c*9 + tap
+        const int col = f - row * BN;
+        rb[i] = *reinterpret_cast<const float4*>(a.wp + (cin0 * 9 + row) * a.cout_pad + n0 + col);
+      }
+    }
+  };
+  auto store_b = [&](float* bs) {
+#pragma unroll
+    for (int i = 0; i < C::B_PER_T; ++i) {
+      const int vi = tid + i * NT;
+      if (vi < C::B_VEC) *reinterpret_cast<float4*>(bs + vi * 4) = rb[i];
+    }
+  };
+
+  f32x16 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // Per-lane LDS column of the A operand for each kx: source column of output x0+l32+kx-1.
+  int acol[3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) acol[kx] = C::C0 + (((x0 + l32 + kx - 1) >> (UP - 1)) - sx0);
+  const int abase = h * SR * RS;                       // lane half h reads channel 2kp+h
+  const int bbase = h * 9 * BN + wn * RN * 32 + l32;
+
+  const int nchunks = (a.Cin + CK - 1) / CK;
+  if (fast) {
+    load_a_fast(0);
+    store_a_fast(As);
+  } else {
+    fill_a_slow(0, As);
+  }
+  load_b(0);
+  store_b(Bs);
+  __syncthreads();
+
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const int buf = kc & 1;
+    const bool more = kc + 1 < nchunks;
+    if (more) {
+      if (fast) load_a_fast((kc + 1) * CK);
+      load_b((kc + 1) * CK);
+    }
+
+    const float* as = As + buf * A_ELEMS + abase;
+    const float* bs = Bs + buf * B_ELEMS + bbase;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int tap = ky * 3 + kx;
+#pragma unroll
+        for (int kp = 0; kp < CK / 2; ++kp) {
+          float av[RM], bv[RN];
+#pragma unroll
+          for (int i = 0; i < RM; ++i) {
+            // output row (within tile) wm*RM+i, tap row ky -> source row in the LDS tile
+            const int orow = wm * RM + i + ky - 1;  // -1 .. TH
+            const int srow = (UP == 1) ? orow + 1 : (orow >> 1) + 1;
+            av[i] = as[(2 * kp * SR + srow) * RS + acol[kx]];
+          }
+#pragma unroll
+          for (int j = 0; j < RN; ++j) bv[j] = bs[(2 * kp * 9 + tap) * BN + j * 32];
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    if (more) {
+      float* an = As + (buf ^ 1) * A_ELEMS;
+      if (fast) store_a_fast(an);
+      else fill_a_slow((kc + 1) * CK, an);
+      store_b(Bs + (buf ^ 1) * B_ELEMS);
+    }
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  const int H = a.H, W = a.W;
+  const int64_t plane = (int64_t)H * W;
+  const bool vec4 = (W & 3) == 0;
+  const int Ho = H >> 1, Wo = W >> 1;
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int co = n0 + (wn * RN + j) * 32 + l32;
+    const bool cok = co < a.Cout;
+    const float bv = (cok && a.bias) ? a.bias[co] : 0.f;
+    const int64_t obase = ((int64_t)n * a.Cout + co) * plane;
+    if (a.y_pre || a.y_act) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int yy = y0 + wm * RM + i;
+        if (!cok || yy >= H) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int xx = x0 + 8 * g + 4 * h;
+          if (xx >= W) continue;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * g + r] + bv;
+          const int64_t off = obase + (int64_t)yy * W + xx;
+          const bool full = vec4 && xx + 3 < W;
+          if (a.y_pre) {
+            if (full) *reinterpret_cast<float4*>(a.y_pre + off) = make_float4(v[0], v[1], v[2], v[3]);
+            else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_pre[off + r] = v[r];
+          }
+          if (a.y_act) {
+            float u[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) u[r] = relu_f(v[r]);
+            if (full) *reinterpret_cast<float4*>(a.y_act + off) = make_float4(u[0], u[1], u[2], u[3]);
+            else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_act[off + r] = u[r];
+          }
+        }
+      }
+    }
+    if (a.y_pool && cok) {
+      const int64_t pbase = ((int64_t)n * a.Cout + co) * Ho * Wo;
+#pragma unroll
+      for (int i = 0; i + 1 < RM; i += 2) {
+        const int py = (y0 + wm * RM + i) >> 1;
+        if (py >= Ho) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int px = (x0 + 8 * g + 4 * h) >> 1;
+          if (px >= Wo) continue;
+          float m[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            m[r] = max_nan(relu_f(acc[i][j][4 * g + r] + bv), relu_f(acc[i + 1][j][4 * g + r] + bv));
+          const float p0 = max_nan(m[0], m[1]), p1 = max_nan(m[2], m[3]);
+          const int64_t off = pbase + (int64_t)py * Wo + px;
+          if (px + 1 < Wo && (Wo & 1) == 0) {
+            *reinterpret_cast<float2*>(a.y_pool + off) = make_float2(p0, p1);
+          } else {
+            a.y_pool[off] = p0;
+            if (px + 1 < Wo) a.y_pool[off + 1] = p1;
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ wp, int cout, int cin,
+                                    int cout_pad, int cin_pad) {
+  const int64_t total = (int64_t)cin_pad * 9 * cout_pad;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(idx % cout_pad);
+    const int64_t rt = idx / cout_pad;
+    const int tap = (int)(rt % 9);
+    const int ci = (int)(rt / 9);
+    wp[idx] = (ci < cin && co < cout) ? w[((int64_t)co * cin + ci) * 9 + tap] : 0.f;
+  }
+}
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+inline int round_up(int a, int b) { return cdiv(a, b) * b; }
+
+template <int WM, int WN, int RM, int RN, int CK, int UP>
+int launch_one(const ConvArgs& a0, hipStream_t s) {
+  using C = Cfg<WM, WN, RM, RN, CK, UP>;
+  ConvArgs a = a0;
+  a.tiles_x = cdiv(a.W, TW);
+  a.tiles_y = cdiv(a.H, C::TH);
+  if (cdiv(a.Cout, C::BN) * C::BN > a.cout_pad) return AST_E_UNSUPPORTED;  // weight-slab reads stay in bounds
+  const int64_t nblk = (int64_t)a.tiles_x * a.tiles_y * a.N;
+  if (nblk >= 0x7fffffff) return AST_E_SHAPE;
+  dim3 grid((unsigned)nblk, (unsigned)cdiv(a.Cout, C::BN));
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)conv3x3_f32_kernel<WM, WN, RM, RN, CK, UP>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((conv3x3_f32_kernel<WM, WN, RM, RN, CK, UP>), grid, dim3(C::NT), C::LDS_BYTES, s, a);
+  return (int)hipGetLastError();
+}
+
+template <int WM, int WN, int RM, int RN, int CK>
+int launch_cfg(const ConvArgs& a, hipStream_t s, int up) {
+  return up == 2 ? launch_one<WM, WN, RM, RN, CK, 2>(a, s) : launch_one<WM, WN, RM, RN, CK, 1>(a, s);
+}
+
+struct CfgEntry {
+  int (*fn)(const ConvArgs&, hipStream_t, int);
+  int bn;
+  int th;
+  int rm;
+};
+
+// Index -> configuration. Keep the table stable (tests/tuner address entries by index).
+const CfgEntry kConfigs[] = {
+    {launch_cfg<4, 1, 2, 2, 8>, 64, 8, 2},   // 0: 8x32 px x 64 ch, CK 8
+    {launch_cfg<4, 1, 2, 2, 4>, 64, 8, 2},   // 1: 8x32 px x 64 ch, CK 4
+    {launch_cfg<2, 2, 4, 2, 4>, 128, 8, 4},  // 2: 8x32 px x 128 ch, CK 4
+    {launch_cfg<2, 2, 2, 2, 8>, 128, 4, 2},  // 3: 4x32 px x 128 ch, CK 8
+    {launch_cfg<4, 1, 4, 2, 4>, 64, 16, 4},  // 4: 16x32 px x 64 ch, CK 4
+};
+constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
+
+int auto_config(int cout, int h, int w) {
+  (void)h;
+  (void)w;
+  if (cout % 128 == 0) return 2;
+  return 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ast_version(void) { return "ast_hip 0.1 gfx950"; }
+
+size_t ast_conv3x3_packed_numel(int cout, int cin) {
+  if (cout <= 0 || cin <= 0) return 0;
+  return (size_t)round_up(cin, kCinAlign) * 9 * (size_t)round_up(cout, kCoutAlign);
+}
+
+int ast_conv3x3_pack_weights_f32(const float* w, float* w_packed, int cout, int cin, void* stream) {
+  if (!w || !w_packed) return AST_E_NULLPTR;
+  if (cout <= 0 || cin <= 0) return AST_E_SHAPE;
+  const int cout_pad = round_up(cout, kCoutAlign), cin_pad = round_up(cin, kCinAlign);
+  const int64_t total = (int64_t)cin_pad * 9 * cout_pad;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, w_packed, cout, cin,
+                     cout_pad, cin_pad);
+  return (int)hipGetLastError();
+}
+
+int ast_conv3x3_num_configs(void) { return kNumConfigs; }
+
+int ast_conv3x3_fwd_f32_cfg(int cfg, const float* x, const float* x2, int n2, const float* w_packed,
+                            const float* bias, float* y_pre, float* y_act, float* y_pool, const float* in_mean,
+                            const float* in_std, int n, int cin, int h_in, int w_in, int cout, int upsample,
+                            int pad_mode, void* stream) {
+  if (!x || !w_packed) return AST_E_NULLPTR;
+  if (n2 < 0 || (n2 > 0 && !x2)) return AST_E_NULLPTR;
+  if (!y_pre && !y_act && !y_pool) return AST_E_NULLPTR;
+  if ((in_mean == nullptr) != (in_std == nullptr)) return AST_E_NULLPTR;
+  if (n <= 0 || cin <= 0 || h_in <= 0 || w_in <= 0 || cout <= 0) return AST_E_SHAPE;
+  if (upsample != 1 && upsample != 2) return AST_E_UNSUPPORTED;
+  if (pad_mode != 0 && pad_mode != 1) return AST_E_UNSUPPORTED;
+  const int H = h_in * upsample, W = w_in * upsample;
+  if (pad_mode == 1 && (H < 2 || W < 2)) return AST_E_SHAPE;  // ReflectionPad2d(1) needs size >= 2
+  if ((int64_t)cin * h_in * w_in >= ((int64_t)1 << 31)) return AST_E_SHAPE;         // per-image offsets are 32-bit
+  if ((int64_t)round_up(cin, kCinAlign) * 9 * round_up(cout, kCoutAlign) >= ((int64_t)1 << 31)) return AST_E_SHAPE;
+  if (cfg < 0) cfg = auto_config(cout, H, W);
+  if (cfg >= kNumConfigs) return AST_E_UNSUPPORTED;
+  const CfgEntry& e = kConfigs[cfg];
+  if (y_pool && (e.rm % 2 != 0)) return AST_E_UNSUPPORTED;
+  if (e.bn > kCoutAlign && (cout % e.bn) != 0) return AST_E_UNSUPPORTED;
+  ConvArgs a{};
+  a.x = x; a.x2 = x2; a.nsplit = n; a.wp = w_packed; a.bias = bias;
+  a.y_pre = y_pre; a.y_act = y_act; a.y_pool = y_pool;
+  a.in_mean = in_mean; a.in_std = in_std;
+  a.N = n + n2; a.Cin = cin; a.Hin = h_in; a.Win = w_in; a.Cout = cout; a.H = H; a.W = W;
+  a.cin_pad = round_up(cin, kCinAlign);
+  a.cout_pad = round_up(cout, kCoutAlign);
+  a.reflect = pad_mode;
+  return e.fn(a, (hipStream_t)stream, upsample);
+}
+
+int ast_conv3x3_fwd_f32(const float* x, const float* w_packed, const float* bias, float* y_pre, float* y_act,
+                        float* y_pool, const float* in_mean, const float* in_std, int n, int cin, int h_in, int w_in,
+                        int cout, int upsample, int pad_mode, void* stream) {
+  return ast_conv3x3_fwd_f32_cfg(-1, x, nullptr, 0, w_packed, bias, y_pre, y_act, y_pool, in_mean, in_std, n, cin, h_in, w_in,
+                                 cout, upsample, pad_mode, stream);
+}
+
+}  // extern "C"

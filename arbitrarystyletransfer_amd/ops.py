@@ -1,0 +1,178 @@
+"""Functional wrappers over the HIP kernels (C ABI in include/ast_hip.h).
+
+Each op takes device tensors, checks shapes/dtypes on the host (a kernel is never launched on a
+shape it does not support), allocates outputs with the PyTorch caching allocator and enqueues the
+kernel on the current HIP stream. No host synchronisation, so sequences of ops can be captured
+into a hipGraph. CPU tensors raise: there is no CPU fallback in the product path.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import HipOpError, check, lib, ptr, stream_ptr
+
+PAD_MODES = {"zeros": 0, "reflect": 1}
+
+
+class LaunchTimer:
+    """Records a pair of HIP events around every conv3x3 launch, on the launch stream, while
+    active (bench.py's live roofline measurement). Use as a context manager."""
+
+    active = None
+
+    def __init__(self):
+        self.records = []  # (tag, flops, start_event, end_event)
+
+    def __enter__(self):
+        LaunchTimer.active = self
+        return self
+
+    def __exit__(self, *exc):
+        LaunchTimer.active = None
+
+    def results(self):
+        """[(tag, flops, milliseconds)] — call after synchronising the device."""
+        return [(tag, fl, s.elapsed_time(e)) for tag, fl, s, e in self.records]
+
+
+def _timed(tag, flops, device, launch):
+    t = LaunchTimer.active
+    if t is None:
+        return launch()
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    stream = torch.cuda.current_stream(device)
+    s.record(stream)
+    code = launch()
+    e.record(stream)
+    t.records.append((tag, flops, s, e))
+    return code
+
+
+def _dev(t: torch.Tensor, name: str) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    if t.device.type != "cuda":
+        raise HipOpError(f"{name} is on {t.device}; arbitrarystyletransfer_amd runs on MI355X (HIP) devices only")
+    if t.dtype != torch.float32:
+        raise HipOpError(f"{name} must be float32, got {t.dtype}")
+    return t.contiguous()
+
+
+# ------------------------------------------------------------------------------------------------
+# 3x3 convolution
+# ------------------------------------------------------------------------------------------------
+
+def pack_conv3x3(weight: torch.Tensor) -> torch.Tensor:
+    """Repack a [cout, cin, 3, 3] filter bank into the kernel's [cin_pad][9][cout_pad] layout."""
+    w = _dev(weight, "weight")
+    if w.dim() != 4 or w.shape[2:] != (3, 3):
+        raise HipOpError(f"conv3x3 weight must be [cout, cin, 3, 3], got {tuple(w.shape)}")
+    cout, cin = int(w.shape[0]), int(w.shape[1])
+    L = lib()
+    out = torch.empty(int(L.ast_conv3x3_packed_numel(cout, cin)), device=w.device, dtype=torch.float32)
+    check(L.ast_conv3x3_pack_weights_f32(ptr(w), ptr(out), cout, cin, stream_ptr(w.device)), "pack_conv3x3")
+    return out
+
+
+def conv3x3(x: torch.Tensor, w_packed: torch.Tensor, bias, cout: int, *, upsample: int = 1,
+            pad_mode: str = "zeros", in_mean=None, in_std=None,
+            want_pre: bool = False, want_act: bool = True, want_pool: bool = False, cfg: int = -1,
+            x2: torch.Tensor | None = None):
+    """Fused [Upsample x2] -> pad(1) -> Conv3x3 -> (+bias) -> {pre, ReLU, ReLU+MaxPool2x2}.
+
+    x2 (optional): a second batch with x's C, H, W; outputs hold x's images then x2's (one
+    launch for a content batch and a style batch, no concatenation copy).
+    Returns (pre, act, pool) with None for outputs not requested.
+    """
+    x = _dev(x, "x")
+    if x.dim() != 4:
+        raise HipOpError(f"x must be NCHW, got {tuple(x.shape)}")
+    n1, cin, h_in, w_in = (int(s) for s in x.shape)
+    n2 = 0
+    if x2 is not None:
+        x2 = _dev(x2, "x2")
+        if x2.dim() != 4 or tuple(x2.shape[1:]) != tuple(x.shape[1:]) or x2.device != x.device:
+            raise HipOpError(f"x2 {tuple(x2.shape)} must match x {tuple(x.shape)} in C, H, W")
+        n2 = int(x2.shape[0])
+    n = n1 + n2
+    if w_packed.numel() != int(lib().ast_conv3x3_packed_numel(cout, cin)):
+        raise HipOpError("packed weight does not match (cout, cin)")
+    if bias is not None:
+        bias = _dev(bias, "bias")
+        if bias.numel() != cout:
+            raise HipOpError("bias size mismatch")
+    if (in_mean is None) != (in_std is None):
+        raise HipOpError("in_mean and in_std go together")
+    if in_mean is not None:
+        in_mean, in_std = _dev(in_mean, "in_mean"), _dev(in_std, "in_std")
+        if in_mean.numel() != cin or in_std.numel() != cin:
+            raise HipOpError("normalisation stats must have cin entries")
+    if pad_mode not in PAD_MODES:
+        raise HipOpError(f"pad_mode must be one of {list(PAD_MODES)}")
+    H, W = h_in * upsample, w_in * upsample
+    mk = lambda hh, ww: torch.empty((n, cout, hh, ww), device=x.device, dtype=torch.float32)  # noqa: E731
+    pre = mk(H, W) if want_pre else None
+    act = mk(H, W) if want_act else None
+    pool = mk(H // 2, W // 2) if want_pool else None
+    if pool is not None and (H < 2 or W < 2):
+        raise HipOpError("max-pool needs H, W >= 2")
+    if pre is None and act is None and pool is None:
+        raise HipOpError("conv3x3: no output requested")
+    flops = 2 * n * H * W * cout * cin * 9
+    tag = f"conv3x3 {cin}->{cout} {H}x{W} up{upsample} {pad_mode}"
+    code = _timed(tag, flops, x.device, lambda: lib().ast_conv3x3_fwd_f32_cfg(
+        cfg, ptr(x), ptr(x2), n2, ptr(w_packed), ptr(bias), ptr(pre), ptr(act), ptr(pool), ptr(in_mean),
+        ptr(in_std), n1, cin, h_in, w_in, cout, upsample, PAD_MODES[pad_mode], stream_ptr(x.device)))
+    check(code, "conv3x3")
+    return pre, act, pool
+
+
+# ------------------------------------------------------------------------------------------------
+# Statistics / AdaIN
+# ------------------------------------------------------------------------------------------------
+
+def channel_stats(x: torch.Tensor, unbiased: bool = True, eps: float = 0.0):
+    """Per-(n, c) mean and std over H, W, keepdim (model_util.py:3-8; calc_mean_std with eps)."""
+    x = _dev(x, "x")
+    if x.dim() != 4:
+        raise HipOpError("channel_stats expects NCHW")
+    n, c, h, w = x.shape
+    mean = torch.empty((n, c, 1, 1), device=x.device, dtype=torch.float32)
+    std = torch.empty_like(mean)
+    check(lib().ast_channel_stats_f32(ptr(x), ptr(mean), ptr(std), n * c, h * w, 1 if unbiased else 0,
+                                      float(eps), stream_ptr(x.device)), "channel_stats")
+    return mean, std
+
+
+def adain(content: torch.Tensor, style: torch.Tensor, alpha: float = 1.0, swap_style_stats: bool = True):
+    """AdaIN (models.py:43-51) fused with the alpha blend of models.py:471."""
+    content = _dev(content, "content_map")
+    style = _dev(style, "style_map")
+    if content.dim() != 4 or style.dim() != 4 or content.shape[:2] != style.shape[:2]:
+        raise HipOpError(f"AdaIN needs NCHW maps with equal (N, C): {tuple(content.shape)} vs {tuple(style.shape)}")
+    n, c, hc, wc = (int(s) for s in content.shape)
+    hs, ws = int(style.shape[2]), int(style.shape[3])
+    out = torch.empty_like(content)
+    nbytes = 4 * (2 * content.numel() + style.numel())  # algorithmic: read c, read s, write out
+    check(_timed(f"adain {c}ch {hc}x{wc}", -nbytes, content.device, lambda: lib().ast_adain_f32(
+        ptr(content), ptr(style), ptr(out), n, c, hc, wc, hs, ws, float(alpha), 1 if swap_style_stats else 0,
+        stream_ptr(content.device))), "adain")
+    return out
+
+
+def plane_normalize(x: torch.Tensor, mean: torch.Tensor, std: torch.Tensor):
+    x = _dev(x, "x")
+    mean, std = _dev(mean, "mean"), _dev(std, "std")
+    n, c = x.shape[:2]
+    hw = x.numel() // (n * c)
+    out = torch.empty_like(x)
+    check(lib().ast_plane_normalize_f32(ptr(x), ptr(mean), ptr(std), ptr(out), n * c, hw,
+                                        stream_ptr(x.device)), "plane_normalize")
+    return out
+
+
+def mean_variance_norm(x: torch.Tensor):
+    """models.py:64-68 (unbiased var + 1e-5)."""
+    mean, std = channel_stats(x, unbiased=True, eps=1e-5)
+    return plane_normalize(x, mean, std)

@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Benchmark: stylised images/s for the VGG19-relu4_1 AdaIN forward (BASELINE.json config 2:
+bs=8 per GPU, 512x512, fp32) on MI355X, one process per GPU.
+
+A step = one forward pass over one batch: encode 8 content + 8 style images (one launch per
+conv layer, both batches together), AdaIN + blend, decode 8 images. Inputs and weights are
+synthetic (live-init recipe, arbitrarystyletransfer_amd/synth.py) and resident in HBM before the
+timed region. N > 1 GPUs: each rank stylises its own batch of 8 (the path shards by image, no
+collective on the data path) -> weak scaling; value = all ranks' images / max-over-ranks time.
+
+Prints ONE JSON line (rank 0). Extra objects:
+  roofline      dominant kernel (conv3x3 MFMA-fp32 implicit GEMM, all 18 launches of a step):
+                algorithmic FLOPs / summed kernel time from HIP events recorded on the launch
+                stream during the timed steps, against the 157.3 TF fp32 matrix peak.
+  cpu_baseline  the CPU oracle (oracle/ref_cpu.py, stock torch CPU ops = the reference's CPU
+                path) on a bounded sample (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from arbitrarystyletransfer_amd import models, ops, synth  # noqa: E402
+
+METRIC = "stylised images/sec at 512x512 bs=8, 1->8 MI355X; encoder MFMA %-of-peak"
+PEAK_FP32_MFMA_TF = 157.3       # MI355X_MICROARCH.md: 256 CU x 4 SIMD x 64 FLOP/clk x 2.4 GHz
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=8, help="images per GPU (config 2: 8)")
+    p.add_argument("--size", type=int, default=512)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(os.cpu_count(), OMP_NUM_THREADS or 16)")
+    return p.parse_args()
+
+
+def cpu_baseline(size, seconds, threads):
+    """Time the CPU oracle on single 512^2 pairs until `seconds` of work (at least one pair)."""
+    from oracle import ref_cpu as R
+    torch.set_num_threads(threads)
+    enc = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_encoder_weights(1)[:9]]
+    dec = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_decoder_weights(2)]
+    c = torch.from_numpy(synth.image(777, (1, 3, size, size)))
+    s = torch.from_numpy(synth.image(778, (1, 3, size, size)))
+    with torch.no_grad():
+        R.style_transfer(c[:, :, :64, :64], s[:, :, :64, :64], enc, dec)  # warm-up (small)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            R.style_transfer(c, s, enc, dec)
+            n += 1
+            dt = time.perf_counter() - t0
+            if dt >= seconds or n >= 64:
+                break
+    import platform
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} content+style pair(s) of 1x3x{size}x{size}, VGG relu4_1 -> AdaIN -> decoder, "
+                      f"fp32 torch CPU ({cpu_model}, {platform.machine()}), {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    B, S = args.batch, args.size
+    net = models.AdaINStyleTransfer().to(dev).eval()
+    content = torch.from_numpy(synth.image(777 + 2 * rank, (B, 3, S, S))).to(dev)
+    style = torch.from_numpy(synth.image(778 + 2 * rank, (B, 3, S, S))).to(dev)
+
+    def step():
+        with torch.no_grad():
+            return net(content, style)
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    timer = ops.LaunchTimer()
+    t0 = time.perf_counter()
+    with timer:
+        for _ in range(args.steps):
+            out = step()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out).all(), "non-finite output"
+
+    # ---- live roofline from the per-launch events ----
+    recs = timer.results()
+    conv = [(tag, fl, ms) for tag, fl, ms in recs if tag.startswith("conv3x3")]
+    conv_flops = sum(fl for _, fl, _ in conv)
+    conv_ms = sum(ms for _, _, ms in conv)
+    n_launch = len(conv)
+    avg_ms = conv_ms / n_launch
+    avg_flops = conv_flops / n_launch
+    achieved_tf = avg_flops / (avg_ms * 1e-3) / 1e12
+    # encoder = the first 9 conv launches of every step (conv_1..conv_9 over 2B images)
+    per_step = n_launch // args.steps
+    enc = [r for i, r in enumerate(conv) if i % per_step < 9]
+    enc_main = [r for i, r in enumerate(conv) if 1 <= i % per_step < 9]
+    enc_tf = sum(f for _, f, _ in enc) / (sum(m for _, _, m in enc) * 1e-3) / 1e12
+    enc_main_tf = sum(f for _, f, _ in enc_main) / (sum(m for _, _, m in enc_main) * 1e-3) / 1e12
+    adain = [(tag, -fl, ms) for tag, fl, ms in recs if tag.startswith("adain")]
+    adain_gbs = (sum(b for _, b, _ in adain) / (sum(m for _, _, m in adain) * 1e-3) / 1e9) if adain else None
+
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "conv_traffic.json")
+    if os.path.exists(tpath):
+        try:
+            with open(tpath) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    images = B * world * args.steps
+    result = {
+        "metric": METRIC,
+        "value": images / elapsed,
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (live-init VGG19/decoder weights, U[0,1) images), resident in HBM",
+        "config": {"workload": f"config 2: VGG19-relu4_1 encoder (content+style) -> AdaIN -> mirrored decoder, "
+                               f"bs={B}/GPU {S}x{S} fp32 forward",
+                   "global_batch": B * world, "image_size": S, "parallelism": f"batch-sharded x{world}"},
+        "roofline": {"bound": "mfma", "kernel": "conv3x3_f32_kernel (all conv launches of a step)",
+                     "achieved": achieved_tf, "peak": PEAK_FP32_MFMA_TF, "unit": "TFLOP/s",
+                     "frac": achieved_tf / PEAK_FP32_MFMA_TF, "traffic": traffic,
+                     "avg_launch_ms": avg_ms, "avg_launch_gflop": avg_flops / 1e9,
+                     "encoder_frac": enc_tf / PEAK_FP32_MFMA_TF,
+                     "encoder_conv2_9_frac": enc_main_tf / PEAK_FP32_MFMA_TF,
+                     "adain_gbs": adain_gbs,
+                     "conv_share_of_step": conv_ms / args.steps / (elapsed / args.steps * 1e3)},
+    }
+    if os.environ.get("BENCH_PER_LAYER"):
+        layers = {}
+        for i, (tag, fl, ms) in enumerate(conv):
+            key = f"{i % per_step:02d} {tag}"
+            a = layers.setdefault(key, [0.0, 0.0])
+            a[0] += fl
+            a[1] += ms
+        result["per_layer"] = {k: {"ms": v[1] / args.steps, "tflops": v[0] / (v[1] * 1e-3) / 1e12}
+                               for k, v in sorted(layers.items())}
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        threads = args.cpu_threads or min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+        result["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

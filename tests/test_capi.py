@@ -1,0 +1,87 @@
+"""CPU: the C-ABI library loads and exports exactly what include/ast_hip.h declares; host-side
+argument checks reject bad calls before any launch (no GPU needed: nothing is launched)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from arbitrarystyletransfer_amd import _lib
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "ast_hip.h")
+
+
+def declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    decls = {}
+    for m in re.finditer(r"^\s*(?:const\s+)?[\w\*\s]+?\b(ast_\w+)\s*\(([^)]*)\)\s*;", src, flags=re.M):
+        args = [a.strip() for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
+        decls[m.group(1)] = len(args)
+    return decls
+
+
+def test_header_declares_functions():
+    d = declared()
+    assert "ast_conv3x3_fwd_f32" in d and "ast_adain_f32" in d and "ast_channel_stats_f32" in d
+    assert len(d) >= 8
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    for name in declared():
+        assert hasattr(L, name), f"{name} declared in ast_hip.h but not exported"
+
+
+def test_binding_signatures_match_header():
+    d = declared()
+    assert set(d) == set(_lib.SIGNATURES), set(d) ^ set(_lib.SIGNATURES)
+    for name, nargs in d.items():
+        assert len(_lib.SIGNATURES[name][1]) == nargs, name
+
+
+def test_version_and_configs():
+    L = _lib.lib()
+    assert L.ast_version().startswith(b"ast_hip")
+    assert L.ast_conv3x3_num_configs() >= 1
+
+
+def test_packed_numel():
+    L = _lib.lib()
+    # cin padded to 8, cout padded to 64
+    assert L.ast_conv3x3_packed_numel(64, 3) == 8 * 9 * 64
+    assert L.ast_conv3x3_packed_numel(3, 64) == 64 * 9 * 64
+    assert L.ast_conv3x3_packed_numel(512, 256) == 256 * 9 * 512
+    assert L.ast_conv3x3_packed_numel(0, 3) == 0
+
+
+@pytest.mark.parametrize("call", [
+    # null input
+    lambda L: L.ast_conv3x3_fwd_f32(None, 1, None, 1, None, None, None, None, 1, 3, 8, 8, 64, 1, 0, None),
+    # no output
+    lambda L: L.ast_conv3x3_fwd_f32(1, 1, None, None, None, None, None, None, 1, 3, 8, 8, 64, 1, 0, None),
+    # bad upsample
+    lambda L: L.ast_conv3x3_fwd_f32(1, 1, None, 1, None, None, None, None, 1, 3, 8, 8, 64, 3, 0, None),
+    # bad pad mode
+    lambda L: L.ast_conv3x3_fwd_f32(1, 1, None, 1, None, None, None, None, 1, 3, 8, 8, 64, 1, 7, None),
+    # reflect pad of a 1-pixel image
+    lambda L: L.ast_conv3x3_fwd_f32(1, 1, None, 1, None, None, None, None, 1, 3, 1, 8, 64, 1, 1, None),
+    # BN=128 config with cout not a multiple of 128
+    lambda L: L.ast_conv3x3_fwd_f32_cfg(2, 1, None, 0, 1, None, 1, None, None, None, None, 1, 3, 8, 8, 64, 1, 0, None),
+    # mean without std
+    lambda L: L.ast_conv3x3_fwd_f32(1, 1, None, 1, None, None, 1, None, 1, 3, 8, 8, 64, 1, 0, None),
+    lambda L: L.ast_adain_f32(None, 1, 1, 1, 1, 2, 2, 2, 2, 1.0, 1, None),
+    lambda L: L.ast_adain_f32(1, 1, 1, 0, 1, 2, 2, 2, 2, 1.0, 1, None),
+    lambda L: L.ast_channel_stats_f32(1, 1, 1, 0, 4, 1, 0.0, None),
+])
+def test_argument_errors_rejected_before_launch(call):
+    assert call(_lib.lib()) < 0
+
+
+def test_cpu_tensors_are_rejected():
+    import torch
+    from arbitrarystyletransfer_amd import ops
+    with pytest.raises(_lib.HipOpError):
+        ops.adain(torch.zeros(1, 2, 3, 3), torch.zeros(1, 2, 3, 3))
+    with pytest.raises(_lib.HipOpError):
+        ops.pack_conv3x3(torch.zeros(4, 3, 3, 3))
