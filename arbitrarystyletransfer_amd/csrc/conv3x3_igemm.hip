@@ -87,7 +87,17 @@ struct Cfg {
   static constexpr int LDS_BYTES = 2 * (A_ELEMS + B_ELEMS) * 4;
 };
 
-template <int WM, int WN, int RM, int RN, int CK, int UP>
+// Workgroup -> (spatial tile, output-channel group). The G channel groups of one spatial tile
+// read the same input tile, so they get ids b, b+8, ..., b+8(G-1): dispatched together, and onto
+// one XCD under the observed round-robin placement (speed only, never correctness).
+__device__ __forceinline__ bool decode_block(int id, int ntiles, int groups, int& tile, int& group) {
+  const int xcd = id & 7, rest = id >> 3;
+  group = rest % groups;
+  tile = (rest / groups) * 8 + xcd;
+  return tile < ntiles;
+}
+
+template <int WM, int WN, int RM, int RN, int CK, int UP, bool SWAP>
 __global__ __launch_bounds__(WM * WN * 64, 2) void conv3x3_f32_kernel(ConvArgs a) {
   using C = Cfg<WM, WN, RM, RN, CK, UP>;
   constexpr int NT = C::NT, TH = C::TH, BN = C::BN, SW = C::SW, SR = C::SR, RS = C::RS, QV = C::QV;
@@ -105,14 +115,15 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3x3_f32_kernel(ConvArgs a
   const int h = lane >> 5, l32 = lane & 31;
   const int wm = wave % WM, wn = wave / WM;
 
-  int t = blockIdx.x;
+  int t, grp;
+  if (!decode_block(blockIdx.x, a.tiles_x * a.tiles_y * a.N, (a.Cout + BN - 1) / BN, t, grp)) return;
   const int tx = t % a.tiles_x;
   t /= a.tiles_x;
   const int ty = t % a.tiles_y;
   const int n = t / a.tiles_y;
   const int x0 = tx * TW, y0 = ty * TH;
   const int sx0 = x0 / UP, sy0 = y0 / UP - 1;  // source tile origin (row includes the halo)
-  const int n0 = blockIdx.y * BN;
+  const int n0 = grp * BN;
   const int Hin = a.Hin, Win = a.Win;
   const bool fast = (sx0 + SW <= Win) && ((Win & 3) == 0);  // block-uniform
 
@@ -262,7 +273,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3x3_f32_kernel(ConvArgs a
           for (int i = 0; i < RM; ++i)
 #pragma unroll
             for (int j = 0; j < RN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = SWAP ? __builtin_amdgcn_mfma_f32_32x32x2f32(bv[j], av[i], acc[i][j], 0, 0, 0)
+                               : __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
         }
       }
     }
@@ -280,6 +292,53 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3x3_f32_kernel(ConvArgs a
   const int64_t plane = (int64_t)H * W;
   const bool vec4 = (W & 3) == 0;
   const int Ho = H >> 1, Wo = W >> 1;
+  if constexpr (SWAP) {
+    // C^T: lane l32 = output column x0+l32, register r = channel (r&3)+8(r>>2)+4h of the
+    // 32-channel tile. One dword store per register writes two whole 128-B row segments.
+    const int xx = x0 + l32;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int cbase = n0 + (wn * RN + j) * 32 + 4 * h;
+      float bvr[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = cbase + (r & 3) + 8 * (r >> 2);
+        bvr[r] = (co < a.Cout && a.bias) ? a.bias[co] : 0.f;
+      }
+      if (a.y_pre || a.y_act) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i) {
+          const int yy = y0 + wm * RM + i;
+          if (yy >= H || xx >= W) continue;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int co = cbase + (r & 3) + 8 * (r >> 2);
+            if (co >= a.Cout) continue;
+            const float v = acc[i][j][r] + bvr[r];
+            const int64_t off = ((int64_t)n * a.Cout + co) * plane + (int64_t)yy * W + xx;
+            if (a.y_pre) a.y_pre[off] = v;
+            if (a.y_act) a.y_act[off] = relu_f(v);
+          }
+        }
+      }
+      if (a.y_pool) {
+        const int px = xx >> 1;
+#pragma unroll
+        for (int i = 0; i + 1 < RM; i += 2) {
+          const int py = (y0 + wm * RM + i) >> 1;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int co = cbase + (r & 3) + 8 * (r >> 2);
+            float m = max_nan(relu_f(acc[i][j][r] + bvr[r]), relu_f(acc[i + 1][j][r] + bvr[r]));
+            m = max_nan(m, __shfl_xor(m, 1, 64));  // horizontal neighbour = adjacent lane
+            if ((l32 & 1) == 0 && co < a.Cout && py < Ho && px < Wo)
+              a.y_pool[((int64_t)n * a.Cout + co) * Ho * Wo + (int64_t)py * Wo + px] = m;
+          }
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
     const int co = n0 + (wn * RN + j) * 32 + l32;
@@ -342,6 +401,153 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3x3_f32_kernel(ConvArgs a
   }
 }
 
+// Direct (VALU) 3x3 conv for cout <= 4 — the decoder's final 64->3 conv (models.py:627). As a
+// GEMM its N = 3 would leave >90% of every MFMA tile idle; as a direct conv each thread makes
+// 4 adjacent output pixels x COUT channels, weights are wave-uniform scalar loads, and the kernel
+// is bound by reading its input once from HBM. Same source-tile staging as the MFMA kernel.
+template <int COUT, int UP>
+__global__ __launch_bounds__(256, 3) void conv3x3_smallc_kernel(ConvArgs a) {
+  constexpr int NT = 256, TH = 8, TWS = 128, CK = 4;
+  constexpr int SW = TWS / UP, SR = TH / UP + 2, RS = SW + 8, C0 = 4, QV = SW / 4;
+  constexpr int A_ITEMS = CK * SR * (QV + 2);
+  __shared__ __attribute__((aligned(16))) float As[CK * SR * RS];
+
+  const int tid = threadIdx.x;
+  const int tx = tid & 31, ty = tid >> 5;
+  int t = blockIdx.x;
+  const int bx = t % a.tiles_x;
+  t /= a.tiles_x;
+  const int by = t % a.tiles_y;
+  const int n = t / a.tiles_y;
+  const int x0 = bx * TWS, y0 = by * TH;
+  const int sx0 = x0 / UP, sy0 = y0 / UP - 1;
+  const int Hin = a.Hin, Win = a.Win;
+  const bool fast = (sx0 + SW <= Win) && ((Win & 3) == 0);
+  const float* __restrict__ xin =
+      n < a.nsplit ? a.x + (int64_t)n * a.Cin * Hin * Win : a.x2 + (int64_t)(n - a.nsplit) * a.Cin * Hin * Win;
+  const float* __restrict__ wp = a.wp;
+  const int plane_in = Hin * Win;
+
+  float acc[COUT][4];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[co][j] = 0.f;
+
+  __shared__ __attribute__((aligned(16))) float Ws[CK * 9 * 4];  // [c][tap][co(4)] of this chunk
+  constexpr int A_PER_T = (A_ITEMS + NT - 1) / NT;
+  for (int cin0 = 0; cin0 < a.Cin; cin0 += CK) {
+    float4 ra[A_PER_T];
+    if (fast) {  // issue every global load of the chunk before the barrier, store after it
+#pragma unroll
+      for (int i = 0; i < A_PER_T; ++i) {
+        const int e = tid + i * NT;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < A_ITEMS) {
+          const int q = e % (QV + 2);
+          const int cr = e / (QV + 2);
+          const int r = cr % SR, c = cr / SR;
+          const int cin = cin0 + c;
+          const int sy = src_index<UP>(sy0 + r, Hin, a.reflect);
+          if (cin < a.Cin && sy >= 0) {
+            const float* row = xin + cin * plane_in + sy * Win;
+            if (q < QV) {
+              v = *reinterpret_cast<const float4*>(row + sx0 + 4 * q);
+            } else {
+              const int sx = src_index<UP>(q == QV ? sx0 - 1 : sx0 + SW, Win, a.reflect);
+              if (sx >= 0) v.x = row[sx];
+            }
+          }
+        }
+        ra[i] = v;
+      }
+    }
+    float wv = 0.f;
+    if (tid < CK * 9 * 4) {
+      const int c = tid / 36, rem = tid % 36, tap = rem / 4, co = rem % 4;
+      if (cin0 + c < a.Cin && co < COUT) wv = wp[((cin0 + c) * 9 + tap) * a.cout_pad + co];
+    }
+    __syncthreads();  // previous chunk's reads are done
+    if (tid < CK * 9 * 4) Ws[tid] = wv;
+    if (fast) {
+#pragma unroll
+      for (int i = 0; i < A_PER_T; ++i) {
+        const int e = tid + i * NT;
+        if (e < A_ITEMS) {
+          const int q = e % (QV + 2);
+          float* row = As + (e / (QV + 2)) * RS;
+          if (q < QV) *reinterpret_cast<float4*>(row + C0 + 4 * q) = ra[i];
+          else row[q == QV ? C0 - 1 : C0 + SW] = ra[i].x;
+        }
+      }
+    } else {
+      for (int e = tid; e < CK * SR * (SW + 2); e += NT) {
+        const int col = e % (SW + 2);
+        const int cr = e / (SW + 2);
+        const int r = cr % SR, c = cr / SR;
+        const int cin = cin0 + c;
+        const int sy = src_index<UP>(sy0 + r, Hin, a.reflect);
+        const int sx = src_index<UP>(sx0 - 1 + col, Win, a.reflect);
+        As[cr * RS + C0 - 1 + col] = (cin < a.Cin && sy >= 0 && sx >= 0) ? xin[cin * plane_in + sy * Win + sx] : 0.f;
+      }
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int c = 0; c < CK; ++c) {  // channels past Cin hold zero inputs and zero weights
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int orow = ty + ky - 1;
+        const int srow = (UP == 1) ? orow + 1 : (orow >> 1) + 1;
+        const float* rowp = As + (c * SR + srow) * RS + C0;
+        constexpr int NV = UP == 1 ? 6 : 4;
+        float v[NV];
+        const int base = UP == 1 ? 4 * tx - 1 : 2 * tx - 1;
+#pragma unroll
+        for (int m = 0; m < NV; ++m) v[m] = rowp[base + m];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const float4 w4 = *reinterpret_cast<const float4*>(Ws + (c * 9 + ky * 3 + kx) * 4);  // LDS broadcast
+          const float wco[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+          for (int co = 0; co < COUT; ++co) {
+            const float w = wco[co];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int m = UP == 1 ? j + kx : ((j + kx - 1) >> 1) + 1;
+              acc[co][j] = fmaf(v[m], w, acc[co][j]);
+            }
+          }
+        }
+      }
+    }
+  }
+
+  const int H = a.H, W = a.W;
+  const int yy = y0 + ty, xx = x0 + 4 * tx;
+  if (yy >= H || xx >= W) return;
+  const bool full = ((W & 3) == 0) && xx + 3 < W;
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) {
+    if (co >= a.Cout) break;
+    const float bv = a.bias ? a.bias[co] : 0.f;
+    float v[4], u[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = acc[co][j] + bv;
+      u[j] = relu_f(v[j]);
+    }
+    const int64_t off = (((int64_t)n * a.Cout + co) * H + yy) * W + xx;
+    if (a.y_pre) {
+      if (full) *reinterpret_cast<float4*>(a.y_pre + off) = make_float4(v[0], v[1], v[2], v[3]);
+      else for (int j = 0; j < 4; ++j) if (xx + j < W) a.y_pre[off + j] = v[j];
+    }
+    if (a.y_act) {
+      if (full) *reinterpret_cast<float4*>(a.y_act + off) = make_float4(u[0], u[1], u[2], u[3]);
+      else for (int j = 0; j < 4; ++j) if (xx + j < W) a.y_act[off + j] = u[j];
+    }
+  }
+}
+
 __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ wp, int cout, int cin,
                                     int cout_pad, int cin_pad) {
   const int64_t total = (int64_t)cin_pad * 9 * cout_pad;
@@ -358,53 +564,83 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 inline int round_up(int a, int b) { return cdiv(a, b) * b; }
 
-template <int WM, int WN, int RM, int RN, int CK, int UP>
+template <int WM, int WN, int RM, int RN, int CK, int UP, bool SWAP>
 int launch_one(const ConvArgs& a0, hipStream_t s) {
   using C = Cfg<WM, WN, RM, RN, CK, UP>;
   ConvArgs a = a0;
   a.tiles_x = cdiv(a.W, TW);
   a.tiles_y = cdiv(a.H, C::TH);
   if (cdiv(a.Cout, C::BN) * C::BN > a.cout_pad) return AST_E_UNSUPPORTED;  // weight-slab reads stay in bounds
-  const int64_t nblk = (int64_t)a.tiles_x * a.tiles_y * a.N;
+  const int64_t ntiles = (int64_t)a.tiles_x * a.tiles_y * a.N;
+  const int64_t nblk = (ntiles + 7) / 8 * 8 * cdiv(a.Cout, C::BN);
   if (nblk >= 0x7fffffff) return AST_E_SHAPE;
-  dim3 grid((unsigned)nblk, (unsigned)cdiv(a.Cout, C::BN));
+  auto kern = conv3x3_f32_kernel<WM, WN, RM, RN, CK, UP, SWAP>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv3x3_f32_kernel<WM, WN, RM, RN, CK, UP>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv3x3_f32_kernel<WM, WN, RM, RN, CK, UP>), grid, dim3(C::NT), C::LDS_BYTES, s, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(C::NT), C::LDS_BYTES, s, a);
   return (int)hipGetLastError();
 }
 
-template <int WM, int WN, int RM, int RN, int CK>
+template <int WM, int WN, int RM, int RN, int CK, bool SWAP = false>
 int launch_cfg(const ConvArgs& a, hipStream_t s, int up) {
-  return up == 2 ? launch_one<WM, WN, RM, RN, CK, 2>(a, s) : launch_one<WM, WN, RM, RN, CK, 1>(a, s);
+  return up == 2 ? launch_one<WM, WN, RM, RN, CK, 2, SWAP>(a, s) : launch_one<WM, WN, RM, RN, CK, 1, SWAP>(a, s);
+}
+
+template <int COUT>
+int launch_smallc(const ConvArgs& a0, hipStream_t s, int up) {
+  ConvArgs a = a0;
+  if (a.Cout > COUT || a.y_pool) return AST_E_UNSUPPORTED;
+  a.tiles_x = cdiv(a.W, 128);
+  a.tiles_y = cdiv(a.H, 8);
+  const int64_t nblk = (int64_t)a.tiles_x * a.tiles_y * a.N;
+  if (nblk >= 0x7fffffff) return AST_E_SHAPE;
+  if (up == 2)
+    hipLaunchKernelGGL((conv3x3_smallc_kernel<COUT, 2>), dim3((unsigned)nblk), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv3x3_smallc_kernel<COUT, 1>), dim3((unsigned)nblk), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
 }
 
 struct CfgEntry {
   int (*fn)(const ConvArgs&, hipStream_t, int);
-  int bn;
-  int th;
-  int rm;
+  int bn;        // output channels per workgroup (weight-slab width)
+  int th;        // output rows per workgroup
+  int rm;        // output rows per wave (pool needs an even count)
+  int max_cout;  // 0 = any
 };
 
 // Index -> configuration. Keep the table stable (tests/tuner address entries by index).
 const CfgEntry kConfigs[] = {
-    {launch_cfg<4, 1, 2, 2, 8>, 64, 8, 2},   // 0: 8x32 px x 64 ch, CK 8
-    {launch_cfg<4, 1, 2, 2, 4>, 64, 8, 2},   // 1: 8x32 px x 64 ch, CK 4
-    {launch_cfg<2, 2, 4, 2, 4>, 128, 8, 4},  // 2: 8x32 px x 128 ch, CK 4
-    {launch_cfg<2, 2, 2, 2, 8>, 128, 4, 2},  // 3: 4x32 px x 128 ch, CK 8
-    {launch_cfg<4, 1, 4, 2, 4>, 64, 16, 4},  // 4: 16x32 px x 64 ch, CK 4
+    {launch_cfg<4, 1, 2, 2, 8>, 64, 8, 2, 0},    // 0: 8x32 px x 64 ch, CK 8, 4 waves
+    {launch_cfg<4, 1, 2, 2, 4>, 64, 8, 2, 0},    // 1: 8x32 px x 64 ch, CK 4, 4 waves
+    {launch_cfg<2, 2, 4, 2, 4>, 128, 8, 4, 0},   // 2: 8x32 px x 128 ch, CK 4, 4 waves
+    {launch_cfg<2, 2, 2, 2, 8>, 128, 4, 2, 0},   // 3: 4x32 px x 128 ch, CK 8, 4 waves
+    {launch_cfg<4, 1, 4, 2, 4>, 64, 16, 4, 0},   // 4: 16x32 px x 64 ch, CK 4, 4 waves
+    {launch_cfg<2, 2, 2, 2, 4>, 128, 4, 2, 0},   // 5: 4x32 px x 128 ch, CK 4, 4 waves
+    {launch_cfg<4, 2, 2, 2, 4>, 128, 8, 2, 0},   // 6: 8x32 px x 128 ch, CK 4, 8 waves
+    {launch_cfg<8, 1, 2, 2, 4>, 64, 16, 2, 0},   // 7: 16x32 px x 64 ch, CK 4, 8 waves
+    {launch_cfg<4, 2, 4, 2, 4>, 128, 16, 4, 0},  // 8: 16x32 px x 128 ch, CK 4, 8 waves
+    {launch_cfg<2, 1, 2, 2, 4>, 64, 4, 2, 0},    // 9: 4x32 px x 64 ch, CK 4, 2 waves
+    {launch_smallc<3>, 4, 8, 2, 3},              // 10: direct VALU conv, cout <= 3
+    {launch_smallc<4>, 4, 8, 2, 4},              // 11: direct VALU conv, cout <= 4
+    // swapped operands (C^T: pixels on lanes -> whole-line dword stores)
+    {launch_cfg<8, 1, 2, 2, 4, true>, 64, 16, 2, 0},   // 12: as 7
+    {launch_cfg<4, 2, 2, 2, 4, true>, 128, 8, 2, 0},   // 13: as 6
+    {launch_cfg<4, 2, 4, 2, 4, true>, 128, 16, 4, 0},  // 14: as 8
+    {launch_cfg<4, 1, 2, 2, 4, true>, 64, 8, 2, 0},    // 15: as 1
 };
 constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
-int auto_config(int cout, int h, int w) {
-  (void)h;
-  (void)w;
-  if (cout % 128 == 0) return 2;
-  return 1;
+int auto_config(int cout, int n, int h, int w) {
+  if (cout <= 3) return 10;
+  if (cout <= 4) return 11;
+  // 16x32 px x 64 ch, 8 waves: fastest on every VGG shape measured (profiles/, conv_tuning.json);
+  // the 4-wave 8x32 tile when that leaves too few workgroups to fill 256 CUs.
+  const long tiles = (long)n * cdiv(h, 16) * cdiv(w, 32) * cdiv(cout, 64);
+  return tiles >= 256 ? 7 : 1;
 }
 
 }  // namespace
@@ -446,10 +682,11 @@ int ast_conv3x3_fwd_f32_cfg(int cfg, const float* x, const float* x2, int n2, co
   if (pad_mode == 1 && (H < 2 || W < 2)) return AST_E_SHAPE;  // ReflectionPad2d(1) needs size >= 2
   if ((int64_t)cin * h_in * w_in >= ((int64_t)1 << 31)) return AST_E_SHAPE;         // per-image offsets are 32-bit
   if ((int64_t)round_up(cin, kCinAlign) * 9 * round_up(cout, kCoutAlign) >= ((int64_t)1 << 31)) return AST_E_SHAPE;
-  if (cfg < 0) cfg = auto_config(cout, H, W);
+  if (cfg < 0) cfg = auto_config(cout, n + n2, H, W);
   if (cfg >= kNumConfigs) return AST_E_UNSUPPORTED;
   const CfgEntry& e = kConfigs[cfg];
-  if (y_pool && (e.rm % 2 != 0)) return AST_E_UNSUPPORTED;
+  if (y_pool && (e.rm % 2 != 0 || e.max_cout)) return AST_E_UNSUPPORTED;
+  if (e.max_cout && cout > e.max_cout) return AST_E_UNSUPPORTED;
   if (e.bn > kCoutAlign && (cout % e.bn) != 0) return AST_E_UNSUPPORTED;
   ConvArgs a{};
   a.x = x; a.x2 = x2; a.nsplit = n; a.wp = w_packed; a.bias = bias;

@@ -63,6 +63,25 @@ def _dev(t: torch.Tensor, name: str) -> torch.Tensor:
 # 3x3 convolution
 # ------------------------------------------------------------------------------------------------
 
+_TUNING = None
+
+
+def tuned_config(n, cin, h_in, w_in, cout, up, pad_mode, pool) -> int:
+    """Kernel configuration measured fastest for this shape (scripts/tune_conv.py writes
+    conv_tuning.json); -1 (the library's own heuristic) for shapes never tuned."""
+    global _TUNING
+    if _TUNING is None:
+        import json
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tuning.json")
+        try:
+            with open(path) as f:
+                _TUNING = json.load(f)
+        except (OSError, ValueError):
+            _TUNING = {}
+    k = f"{n}x{cin}x{h_in}x{w_in}->{cout} up{up} {pad_mode}{' pool' if pool else ''}"
+    return int(_TUNING.get(k, -1))
+
 def pack_conv3x3(weight: torch.Tensor) -> torch.Tensor:
     """Repack a [cout, cin, 3, 3] filter bank into the kernel's [cin_pad][9][cout_pad] layout."""
     w = _dev(weight, "weight")
@@ -119,6 +138,8 @@ def conv3x3(x: torch.Tensor, w_packed: torch.Tensor, bias, cout: int, *, upsampl
         raise HipOpError("max-pool needs H, W >= 2")
     if pre is None and act is None and pool is None:
         raise HipOpError("conv3x3: no output requested")
+    if cfg < 0:
+        cfg = tuned_config(n, cin, h_in, w_in, cout, upsample, pad_mode, want_pool)
     flops = 2 * n * H * W * cout * cin * 9
     tag = f"conv3x3 {cin}->{cout} {H}x{W} up{upsample} {pad_mode}"
     code = _timed(tag, flops, x.device, lambda: lib().ast_conv3x3_fwd_f32_cfg(

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Sweep every conv3x3 kernel configuration over the layer shapes of the benchmarked path and
+write the fastest per shape to arbitrarystyletransfer_amd/conv_tuning.json (read by ops.conv3x3).
+
+Each (shape, config) is timed with HIP events on the launch stream: 2 warm-up launches, then the
+median of 5. Configurations a shape does not support are rejected on the host (no launch).
+"""
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from arbitrarystyletransfer_amd import ops, synth  # noqa: E402
+from arbitrarystyletransfer_amd._lib import lib  # noqa: E402
+
+# (n, cin, h_in, w_in, cout, up, pad, pool) of the bench step (config 2, B=8 -> encoder sees 16)
+ENC = [(3, 64, 512, False), (64, 64, 512, True), (64, 128, 256, False), (128, 128, 256, True),
+       (128, 256, 128, False), (256, 256, 128, False), (256, 256, 128, False), (256, 256, 128, True),
+       (256, 512, 64, False)]
+DEC = [(512, 256, 64, 1), (256, 256, 64, 2), (256, 256, 128, 1), (256, 256, 128, 1), (256, 128, 128, 1),
+       (128, 128, 128, 2), (128, 64, 256, 1), (64, 64, 256, 2), (64, 3, 512, 1)]
+
+
+def shapes(batch):
+    out = []
+    for cin, cout, s, pool in ENC:
+        out.append((2 * batch, cin, s, s, cout, 1, "zeros", pool))
+    for cin, cout, s, up in DEC:
+        out.append((batch, cin, s, s, cout, up, "reflect", False))
+    return out
+
+
+def key(n, cin, h, w, cout, up, pad, pool):
+    return f"{n}x{cin}x{h}x{w}->{cout} up{up} {pad}{' pool' if pool else ''}"
+
+
+def time_cfg(cfg, x, wp, b, cout, up, pad, pool):
+    args = dict(upsample=up, pad_mode=pad, want_pre=False, want_act=not pool, want_pool=pool, cfg=cfg)
+    try:
+        ops.conv3x3(x, wp, b, cout, **args)
+    except Exception as e:
+        if "unsupported" in str(e):
+            return None
+        raise
+    for _ in range(2):
+        ops.conv3x3(x, wp, b, cout, **args)
+    ts = []
+    for _ in range(5):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        ops.conv3x3(x, wp, b, cout, **args)
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    return statistics.median(ts)
+
+
+def main():
+    batch = int(os.environ.get("TUNE_BATCH", "8"))
+    dev = torch.device("cuda:0")
+    ncfg = lib().ast_conv3x3_num_configs()
+    table = {}
+    path = os.path.join(ROOT, "arbitrarystyletransfer_amd", "conv_tuning.json")
+    if os.path.exists(path):
+        table = json.load(open(path))
+    report = []
+    for shp in shapes(batch):
+        n, cin, h, w, cout, up, pad, pool = shp
+        x = torch.from_numpy(synth.image(5, (n, cin, h, w))).to(dev)
+        wt = torch.from_numpy(synth.conv_weight(6, cout, cin, 3)).to(dev)
+        wp = ops.pack_conv3x3(wt)
+        b = torch.zeros(cout, device=dev)
+        flops = 2 * n * h * up * w * up * cout * cin * 9
+        res = {}
+        for cfg in range(ncfg):
+            t = time_cfg(cfg, x, wp, b, cout, up, pad, pool)
+            if t is not None:
+                res[cfg] = t
+        best = min(res, key=res.get)
+        k = key(*shp)
+        table[k] = best
+        row = {"shape": k, "best": best, "ms": res[best], "tflops": flops / res[best] / 1e9,
+               "all_ms": {str(c): round(t, 4) for c, t in res.items()}}
+        report.append(row)
+        print(json.dumps(row), flush=True)
+        del x, wt, wp
+    with open(path, "w") as f:
+        json.dump(table, f, indent=1, sort_keys=True)
+    extra = os.environ.get("TUNE_COPY")  # gpurun only returns gpurun_out/: keep a copy there
+    if extra:
+        with open(extra, "w") as f:
+            json.dump(table, f, indent=1, sort_keys=True)
+    tot = sum(r["ms"] for r in report)
+    print(json.dumps({"total_ms_best": tot}))
+
+
+if __name__ == "__main__":
+    main()
