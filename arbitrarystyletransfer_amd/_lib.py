@@ -17,6 +17,8 @@ _c_float_p = ctypes.c_void_p
 _i = ctypes.c_int
 _ll = ctypes.c_longlong
 _p = ctypes.c_void_p
+_f = ctypes.c_float
+_d = ctypes.c_double
 
 # name -> (restype, argtypes); must match include/ast_hip.h exactly (tests/test_capi.py checks it)
 SIGNATURES = {
@@ -29,6 +31,26 @@ SIGNATURES = {
     "ast_channel_stats_f32": (_i, [_p, _p, _p, _ll, _ll, _i, ctypes.c_float, _p]),
     "ast_adain_f32": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, ctypes.c_double, _i, _p]),
     "ast_plane_normalize_f32": (_i, [_p, _p, _p, _p, _ll, _ll, _p]),
+    "ast_conv3x3_pack_weights_ex_f32": (_i, [_p, _p, _i, _i, _i, _p, _p]),
+    "ast_conv_act_backward_f32": (_i, [_p, _p, _p, _p, _p, _ll, _i, _i, _p]),
+    "ast_relu_mask_f32": (_i, [_p, _p, _p, _ll, _p]),
+    "ast_conv3x3_dgrad_border_f32": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _p]),
+    "ast_pad_up_adjoint_f32": (_i, [_p, _p, _p, _p, _ll, _i, _i, _i, _p]),
+    "ast_conv3x3_wgrad_f32": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "ast_gram_f32": (_i, [_p, _p, _i, _i, _ll, _f, _p]),
+    "ast_gram_backward_f32": (_i, [_p, _p, _p, _p, _p, _i, _i, _ll, _f, _p, _i, _p]),
+    "ast_mvn_huber_f32": (_i, [_p, _p, _ll, _ll, _f, _p, _p, _p, _i, _p]),
+    "ast_huber_f32": (_i, [_p, _p, _ll, _f, _p, _p, _p, _i, _p]),
+    "ast_style_moments_f32": (_i, [_p, _p, _ll, _ll, _f, _p, _p, _p, _p, _p, _p]),
+    "ast_gram_huber_f32": (_i, [_p, _p, _ll, _f, _p, _p, _p, _p]),
+    "ast_tv_loss_f32": (_i, [_p, _ll, _i, _i, _f, _p, _p, _p, _i, _p]),
+    "ast_mvn_backward_f32": (_i, [_p, _p, _p, _ll, _ll, _f, _p]),
+    "ast_channel_stats_backward_f32": (_i, [_p, _p, _p, _p, _p, _p, _ll, _ll, _i, _i, _p]),
+    "ast_optim_table_bytes": (ctypes.c_size_t, [_i]),
+    "ast_optim_build_table": (_ll, [_p, _i, _p, _p, _p, _p, _p]),
+    "ast_grad_norm_f32": (_i, [_p, _i, _ll, _p, _f, _p, _p]),
+    "ast_grad_scale_f32": (_i, [_p, _i, _ll, _p, _p]),
+    "ast_adam_step_f32": (_i, [_p, _i, _ll, _p, _d, _d, _d, _d, _i, _p]),
 }
 
 ERRORS = {-1: "null pointer", -2: "bad shape", -3: "unsupported configuration"}

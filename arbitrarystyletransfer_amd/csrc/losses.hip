@@ -1,0 +1,496 @@
+// Style-transfer losses for gfx950: losses.py gram_matrix (105-109), compute_content_loss
+// (124-126), compute_style_loss (128-139), tv_loss (90-103), with mean_variance_norm
+// (models.py:64-68) fused into the content term. Each loss kernel produces its value (atomically
+// added into a device scalar) and, when asked, the input gradient, so the training step needs no
+// separate backward pass through PyTorch.
+//
+//  * gram: batched fp32 MFMA GEMM G[b] = s·F[b]F[b]^T (F = C x HW), split-K over HW with fp32
+//    atomics into G (C <= 512, HW up to 512^2: few output tiles, very long K).
+//  * gram backward: dF[b] (+)= s·(dG+dG^T)[b]·F[b] + ra[b,i]·F[b][i,:] + rb[b,i] — the GEMM
+//    epilogue also adds the mean/std-term gradients of compute_style_loss (per-plane affine in F).
+//  * Huber: delta = 1, reduction 'mean' (F.huber_loss default).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/ast_hip.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ float huber(float d) {
+  const float a = fabsf(d);
+  return a < 1.f ? 0.5f * d * d : a - 0.5f;
+}
+__device__ __forceinline__ float huber_grad(float d) { return d < -1.f ? -1.f : (d > 1.f ? 1.f : d); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// 256-thread block sum; every thread receives the total.
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+__device__ void plane_mean_std(const float* __restrict__ p, int64_t n, float eps, float* sh, float& mean, float& sd) {
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += kThreads) s += p[i];
+  mean = block_sum(s, sh) / (float)n;
+  float q = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += kThreads) {
+    const float d = p[i] - mean;
+    q += d * d;
+  }
+  sd = sqrtf(block_sum(q, sh) / (float)(n - 1) + eps);
+}
+
+__device__ __forceinline__ float gs(const float* g) { return g ? *g : 1.f; }
+
+// ------------------------------------------------------------------------------------------
+// Content term: w * huber(mvn(x), mvn(y)) (mean over all elements), dx += d/dx.
+// mvn z = (x-mu)/sigma, sigma = sqrt(var_unbiased + 1e-5). With g = dL/dz:
+//   dx = (g - mean(g) - z * sum(g z)/(N-1)) / sigma.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void mvn_huber_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                             int64_t hw, float inv_numel, float w,
+                                                             const float* __restrict__ gscale, float* loss,
+                                                             float* __restrict__ dx, int accumulate) {
+  __shared__ float sh[4];
+  const int64_t p = blockIdx.x;
+  const float* xp = x + p * hw;
+  const float* yp = y + p * hw;
+  float mx, sx, my, sy;
+  plane_mean_std(xp, hw, 1e-5f, sh, mx, sx);
+  plane_mean_std(yp, hw, 1e-5f, sh, my, sy);
+  float sh_ = 0.f, sg = 0.f, sgz = 0.f;
+  for (int64_t i = threadIdx.x; i < hw; i += kThreads) {
+    const float z = (xp[i] - mx) / sx;
+    const float d = z - (yp[i] - my) / sy;
+    sh_ += huber(d);
+    const float g = huber_grad(d);
+    sg += g;
+    sgz += g * z;
+  }
+  const float H = block_sum(sh_, sh);
+  if (threadIdx.x == 0 && loss) atomicAdd(loss, w * H * inv_numel);
+  if (!dx) return;
+  const float G = block_sum(sg, sh);
+  const float GZ = block_sum(sgz, sh);
+  const float c = w * inv_numel * gs(gscale);
+  const float gmean = G / (float)hw, gz = GZ / (float)(hw - 1);
+  float* dp = dx + p * hw;
+  for (int64_t i = threadIdx.x; i < hw; i += kThreads) {
+    const float z = (xp[i] - mx) / sx;
+    const float d = z - (yp[i] - my) / sy;
+    const float v = c * (huber_grad(d) - gmean - z * gz) / sx;
+    dp[i] = accumulate ? dp[i] + v : v;
+  }
+}
+
+// Backward of mean_variance_norm alone: dx = (g - mean(g) - z*sum(g z)/(N-1)) / sigma.
+__global__ __launch_bounds__(kThreads) void mvn_backward_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                                float* __restrict__ dx, int64_t hw, float eps) {
+  __shared__ float sh[4];
+  const int64_t p = blockIdx.x;
+  const float* xp = x + p * hw;
+  const float* gp = g + p * hw;
+  float m, sd;
+  plane_mean_std(xp, hw, eps, sh, m, sd);
+  float sg = 0.f, sgz = 0.f;
+  for (int64_t i = threadIdx.x; i < hw; i += kThreads) {
+    const float gi = gp[i];
+    sg += gi;
+    sgz += gi * (xp[i] - m) / sd;
+  }
+  const float G = block_sum(sg, sh) / (float)hw;
+  const float GZ = block_sum(sgz, sh) / (float)(hw - 1);
+  float* dp = dx + p * hw;
+  for (int64_t i = threadIdx.x; i < hw; i += kThreads) dp[i] = (gp[i] - G - (xp[i] - m) / sd * GZ) / sd;
+}
+
+// Backward of channel_stats / calc_mean_std: dx = dmean/N + dstd*(x-mean)/((N-unbiased)*std).
+__global__ void stats_backward_kernel(const float* __restrict__ x, const float* __restrict__ mean,
+                                      const float* __restrict__ sd, const float* __restrict__ dmean,
+                                      const float* __restrict__ dsd, float* __restrict__ dx, int64_t hw, int64_t n,
+                                      int unbiased, int accumulate) {
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    const int64_t p = i / hw;
+    float v = 0.f;
+    if (dmean) v += dmean[p] / (float)hw;
+    if (dsd) v += dsd[p] * (x[i] - mean[p]) / ((float)(hw - unbiased) * sd[p]);
+    dx[i] = accumulate ? dx[i] + v : v;
+  }
+}
+
+// Plain Huber (compute_content_loss on raw tensors): loss += w*mean(huber(x-y)), dx (+)= grad.
+__global__ void huber_kernel(const float* __restrict__ x, const float* __restrict__ y, int64_t n, float inv_numel,
+                             float w, const float* __restrict__ gscale, float* loss, float* __restrict__ dx,
+                             int accumulate) {
+  __shared__ float sh[4];
+  const float c = w * inv_numel * gs(gscale);
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    const float d = x[i] - y[i];
+    s += huber(d);
+    if (dx) {
+      const float v = c * huber_grad(d);
+      dx[i] = accumulate ? dx[i] + v : v;
+    }
+  }
+  const float t = block_sum(s, sh);
+  if (threadIdx.x == 0 && loss) atomicAdd(loss, w * t * inv_numel);
+}
+
+// ------------------------------------------------------------------------------------------
+// Style mean/std terms. stats[p] = (mu_x, sd_x, mu_y, sd_y) (unbiased, no eps = channel_stats).
+// loss += w*1.25*(mean huber(mu_x-mu_y) + mean huber(sd_x-sd_y)) over the B*C planes;
+// per-plane gradient dx = ra*x + rb with ra = dsd/((N-1) sd), rb = dmu/N - ra*mu.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void style_stats_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                               int64_t hw, float* __restrict__ stats) {
+  __shared__ float sh[4];
+  const int64_t p = blockIdx.x;
+  float mx, sx, my, sy;
+  plane_mean_std(x + p * hw, hw, 0.f, sh, mx, sx);
+  plane_mean_std(y + p * hw, hw, 0.f, sh, my, sy);
+  if (threadIdx.x == 0) {
+    stats[4 * p + 0] = mx;
+    stats[4 * p + 1] = sx;
+    stats[4 * p + 2] = my;
+    stats[4 * p + 3] = sy;
+  }
+}
+
+__global__ void style_moment_loss_kernel(const float* __restrict__ stats, int64_t planes, int64_t hw, float w,
+                                         const float* __restrict__ gscale, float* loss, float* __restrict__ ra,
+                                         float* __restrict__ rb) {
+  __shared__ float sh[4];
+  const float inv = 1.f / (float)planes;
+  const float c = w * 1.25f * inv * gs(gscale);
+  float s = 0.f;
+  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < planes; p += (int64_t)gridDim.x * kThreads) {
+    const float mx = stats[4 * p], sx = stats[4 * p + 1], my = stats[4 * p + 2], sy = stats[4 * p + 3];
+    s += huber(mx - my) + huber(sx - sy);
+    if (ra) {
+      const float dmu = c * huber_grad(mx - my), dsd = c * huber_grad(sx - sy);
+      const float a = dsd / ((float)(hw - 1) * sx);
+      ra[p] = a;
+      rb[p] = dmu / (float)hw - a * mx;
+    }
+  }
+  const float t = block_sum(s, sh);
+  if (threadIdx.x == 0 && loss) atomicAdd(loss, w * 1.25f * t * inv);
+}
+
+// Gram huber: loss += w*10*mean(huber(Gx-Gy)); dG = w*10*huber'(Gx-Gy)/numel (gscale'd).
+__global__ void gram_huber_kernel(const float* __restrict__ gx, const float* __restrict__ gy, int64_t n, float w,
+                                  const float* __restrict__ gscale, float* loss, float* __restrict__ dg) {
+  __shared__ float sh[4];
+  const float inv = 1.f / (float)n;
+  const float c = w * 10.f * inv * gs(gscale);
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    const float d = gx[i] - gy[i];
+    s += huber(d);
+    if (dg) dg[i] = c * huber_grad(d);
+  }
+  const float t = block_sum(s, sh);
+  if (threadIdx.x == 0 && loss) atomicAdd(loss, w * 10.f * t * inv);
+}
+
+// ------------------------------------------------------------------------------------------
+// TV: loss += w * (sum (x[.., j]-x[.., j+1])^2 + sum (x[i, ..]-x[i+1, ..])^2); dx (+)= grad.
+// ------------------------------------------------------------------------------------------
+__global__ void tv_kernel(const float* __restrict__ x, int64_t planes, int H, int W, float w,
+                          const float* __restrict__ gscale, float* loss, float* __restrict__ dx, int accumulate) {
+  __shared__ float sh[4];
+  const int64_t n = planes * H * W;
+  const float c = 2.f * w * gs(gscale);
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    const int j = (int)(i % W);
+    const int r = (int)((i / W) % H);
+    const float v = x[i];
+    float g = 0.f;
+    if (j + 1 < W) {
+      const float d = v - x[i + 1];
+      s += d * d;
+      g += d;
+    }
+    if (j > 0) g -= x[i - 1] - v;
+    if (r + 1 < H) {
+      const float d = v - x[i + W];
+      s += d * d;
+      g += d;
+    }
+    if (r > 0) g -= x[i - W] - v;
+    if (dx) dx[i] = accumulate ? dx[i] + c * g : c * g;
+  }
+  const float t = block_sum(s, sh);
+  if (threadIdx.x == 0 && loss) atomicAdd(loss, w * t);
+}
+
+// ------------------------------------------------------------------------------------------
+// Gram forward: G[b][i][j] += s * sum_k F[b][i][k] F[b][j][k], k-range split over blockIdx.y.
+// 64x64 output tile, 4 waves (2x2 of 32x32), BK = 32; F tiles transposed into LDS [k][row].
+// ------------------------------------------------------------------------------------------
+constexpr int GT = 64, GBK = 32;
+
+__global__ __launch_bounds__(256) void gram_kernel(const float* __restrict__ F, float* __restrict__ G, int C,
+                                                   int64_t K, int64_t kchunk, float s) {
+  __shared__ float As[GBK][GT + 4];
+  __shared__ float Bs[GBK][GT + 4];
+  const int tiles = (C + GT - 1) / GT;
+  const int ti = blockIdx.x % tiles, tj = blockIdx.x / tiles;
+  const int b = blockIdx.z;
+  const int64_t k0 = (int64_t)blockIdx.y * kchunk;
+  const int64_t k1 = min(K, k0 + kchunk);
+  const float* Fb = F + (int64_t)b * C * K;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int wi = wave & 1, wj = wave >> 1;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const bool vec = ((K & 3) == 0) && ((k0 & 3) == 0);
+  for (int64_t kb = k0; kb < k1; kb += GBK) {
+    // 64 rows x 32 k for each operand: 512 float4 each -> 2 per thread per operand
+#pragma unroll
+    for (int rep = 0; rep < 2; ++rep) {
+      const int e = tid + rep * 256;  // 0..511
+      const int row = e >> 3, kq = (e & 7) * 4;
+      const int ri = ti * GT + row, rj = tj * GT + row;
+      float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+      const int64_t kk = kb + kq;
+      if (vec && kk + 3 < k1) {
+        if (ri < C) va = *reinterpret_cast<const float4*>(Fb + (int64_t)ri * K + kk);
+        if (rj < C) vb = *reinterpret_cast<const float4*>(Fb + (int64_t)rj * K + kk);
+      } else {
+        float ta[4] = {0.f, 0.f, 0.f, 0.f}, tb[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < 4; ++q) {
+          if (kk + q < k1) {
+            if (ri < C) ta[q] = Fb[(int64_t)ri * K + kk + q];
+            if (rj < C) tb[q] = Fb[(int64_t)rj * K + kk + q];
+          }
+        }
+        va = make_float4(ta[0], ta[1], ta[2], ta[3]);
+        vb = make_float4(tb[0], tb[1], tb[2], tb[3]);
+      }
+      As[kq + 0][row] = va.x; As[kq + 1][row] = va.y; As[kq + 2][row] = va.z; As[kq + 3][row] = va.w;
+      Bs[kq + 0][row] = vb.x; Bs[kq + 1][row] = vb.y; Bs[kq + 2][row] = vb.z; Bs[kq + 3][row] = vb.w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kp = 0; kp < GBK / 2; ++kp) {
+      const float a = As[2 * kp + h][wi * 32 + l32];
+      const float bv = Bs[2 * kp + h][wj * 32 + l32];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  float* Gb = G + (int64_t)b * C * C;
+  const int j = tj * GT + wj * 32 + l32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = ti * GT + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (i < C && j < C) atomicAdd(Gb + (int64_t)i * C + j, s * acc[r]);
+  }
+}
+
+// Gram backward: dF[b][i][n] (+)= s * sum_k (dG[k][i] + dG[i][k]) F[b][k][n] + ra[b,i] F[b][i][n] + rb[b,i].
+// Output tile 64 (i) x 128 (n); 4 waves 2x2, each 32 x 64; BK = 16.
+constexpr int BI = 64, BNN = 128, BBK = 16;
+
+__global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__ F, const float* __restrict__ dG,
+                                                       float* __restrict__ dF, const float* __restrict__ ra,
+                                                       const float* __restrict__ rb, int C, int64_t HW, float s,
+                                                       const float* __restrict__ gscale, int accumulate) {
+  __shared__ float As[BBK][BI + 4];   // S^T tile: [k][i]
+  __shared__ float Bs[BBK][BNN + 4];  // F tile:  [k][n]
+  const int b = blockIdx.z;
+  const int ti = blockIdx.y;
+  const int64_t n0 = (int64_t)blockIdx.x * BNN;
+  const float* Fb = F + (int64_t)b * C * HW;
+  const float* dGb = dG + (int64_t)b * C * C;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int wi = wave & 1, wn = wave >> 1;
+  f32x16 acc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+  for (int k0 = 0; k0 < C; k0 += BBK) {
+    // S tile: 16 k x 64 i = 1024 entries, 4 per thread
+#pragma unroll
+    for (int rep = 0; rep < 4; ++rep) {
+      const int e = tid + rep * 256;
+      const int kk = e >> 6, ii = e & 63;
+      const int k = k0 + kk, i = ti * BI + ii;
+      float v = 0.f;
+      if (k < C && i < C) v = dGb[(int64_t)k * C + i] + dGb[(int64_t)i * C + k];
+      As[kk][ii] = v;
+    }
+    // F tile: 16 k x 128 n = 512 float4 -> 2 per thread
+#pragma unroll
+    for (int rep = 0; rep < 2; ++rep) {
+      const int e = tid + rep * 256;
+      const int kk = e >> 5, nq = (e & 31) * 4;
+      const int k = k0 + kk;
+      const int64_t nn = n0 + nq;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < C) {
+        const float* row = Fb + (int64_t)k * HW;
+        if (((HW & 3) == 0) && nn + 3 < HW) {
+          v = *reinterpret_cast<const float4*>(row + nn);
+        } else {
+          float t[4] = {0.f, 0.f, 0.f, 0.f};
+          for (int q = 0; q < 4; ++q) if (nn + q < HW) t[q] = row[nn + q];
+          v = make_float4(t[0], t[1], t[2], t[3]);
+        }
+      }
+      *reinterpret_cast<float4*>(&Bs[kk][nq]) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kp = 0; kp < BBK / 2; ++kp) {
+      const float a = As[2 * kp + h][wi * 32 + l32];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float bv = Bs[2 * kp + h][wn * 64 + q * 32 + l32];
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc[q], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  float* dFb = dF + (int64_t)b * C * HW;
+  const float g = gs(gscale);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int64_t n = n0 + wn * 64 + q * 32 + l32;
+    if (n >= HW) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = ti * BI + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (i >= C) continue;
+      const int64_t off = (int64_t)i * HW + n;
+      float v = s * acc[q][r];
+      if (ra) v += ra[(int64_t)b * C + i] * Fb[off] + rb[(int64_t)b * C + i];
+      v *= g;
+      dFb[off] = accumulate ? dFb[off] + v : v;
+    }
+  }
+}
+
+int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, 4096)); }
+
+}  // namespace
+
+extern "C" {
+
+int ast_gram_f32(const float* feat, float* gram, int n, int c, long long hw, float scale, void* stream) {
+  if (!feat || !gram) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hw <= 0 || n > 65535) return AST_E_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(gram, 0, sizeof(float) * (size_t)n * c * c, s);
+  if (e != hipSuccess) return (int)e;
+  const int tiles = (c + GT - 1) / GT;
+  // split K so that the launch has >= ~1024 workgroups, chunks a multiple of GBK
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>((hw + 1023) / 1024, 1024 / std::max(1, n * tiles * tiles) + 1));
+  int64_t kchunk = (hw + splits - 1) / splits;
+  kchunk = (kchunk + GBK - 1) / GBK * GBK;
+  splits = (hw + kchunk - 1) / kchunk;
+  if (splits > 65535) return AST_E_SHAPE;
+  hipLaunchKernelGGL(gram_kernel, dim3(tiles * tiles, (unsigned)splits, n), dim3(256), 0, s, feat, gram, c,
+                     (int64_t)hw, kchunk, scale);
+  return (int)hipGetLastError();
+}
+
+int ast_gram_backward_f32(const float* feat, const float* dgram, float* dfeat, const float* row_a, const float* row_b,
+                          int n, int c, long long hw, float scale, const float* gscale, int accumulate,
+                          void* stream) {
+  if (!feat || !dgram || !dfeat) return AST_E_NULLPTR;
+  if ((row_a == nullptr) != (row_b == nullptr)) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hw <= 0 || n > 65535) return AST_E_SHAPE;
+  const int64_t nb = (hw + BNN - 1) / BNN;
+  if (nb > 0x7fffffff) return AST_E_SHAPE;
+  hipLaunchKernelGGL(gram_bwd_kernel, dim3((unsigned)nb, (c + BI - 1) / BI, n), dim3(256), 0, (hipStream_t)stream,
+                     feat, dgram, dfeat, row_a, row_b, c, (int64_t)hw, scale, gscale, accumulate ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int ast_mvn_huber_f32(const float* x, const float* y, long long planes, long long hw, float weight,
+                      const float* gscale, float* loss, float* dx, int accumulate, void* stream) {
+  if (!x || !y) return AST_E_NULLPTR;
+  if (planes <= 0 || hw <= 1 || planes > 0x7fffffffLL) return AST_E_SHAPE;
+  hipLaunchKernelGGL(mvn_huber_kernel, dim3((unsigned)planes), dim3(kThreads), 0, (hipStream_t)stream, x, y,
+                     (int64_t)hw, (float)(1.0 / ((double)planes * hw)), weight, gscale, loss, dx, accumulate ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int ast_mvn_backward_f32(const float* x, const float* g, float* dx, long long planes, long long hw, float eps,
+                         void* stream) {
+  if (!x || !g || !dx) return AST_E_NULLPTR;
+  if (planes <= 0 || hw <= 1 || planes > 0x7fffffffLL) return AST_E_SHAPE;
+  hipLaunchKernelGGL(mvn_backward_kernel, dim3((unsigned)planes), dim3(kThreads), 0, (hipStream_t)stream, x, g, dx,
+                     (int64_t)hw, eps);
+  return (int)hipGetLastError();
+}
+
+int ast_channel_stats_backward_f32(const float* x, const float* mean, const float* std, const float* dmean,
+                                   const float* dstd, float* dx, long long planes, long long hw, int unbiased,
+                                   int accumulate, void* stream) {
+  if (!x || !mean || !std || !dx) return AST_E_NULLPTR;
+  if (planes <= 0 || hw <= 0) return AST_E_SHAPE;
+  hipLaunchKernelGGL(stats_backward_kernel, dim3(grid_for(planes * hw)), dim3(kThreads), 0, (hipStream_t)stream, x,
+                     mean, std, dmean, dstd, dx, (int64_t)hw, (int64_t)planes * hw, unbiased ? 1 : 0,
+                     accumulate ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int ast_huber_f32(const float* x, const float* y, long long n, float weight, const float* gscale, float* loss,
+                  float* dx, int accumulate, void* stream) {
+  if (!x || !y) return AST_E_NULLPTR;
+  if (n <= 0) return AST_E_SHAPE;
+  hipLaunchKernelGGL(huber_kernel, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, x, y, (int64_t)n,
+                     (float)(1.0 / (double)n), weight, gscale, loss, dx, accumulate ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int ast_style_moments_f32(const float* x, const float* y, long long planes, long long hw, float weight,
+                          const float* gscale, float* stats, float* loss, float* row_a, float* row_b, void* stream) {
+  if (!x || !y || !stats) return AST_E_NULLPTR;
+  if ((row_a == nullptr) != (row_b == nullptr)) return AST_E_NULLPTR;
+  if (planes <= 0 || hw <= 0 || planes > 0x7fffffffLL) return AST_E_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(style_stats_kernel, dim3((unsigned)planes), dim3(kThreads), 0, s, x, y, (int64_t)hw, stats);
+  hipLaunchKernelGGL(style_moment_loss_kernel, dim3(grid_for(planes)), dim3(kThreads), 0, s, stats, (int64_t)planes,
+                     (int64_t)hw, weight, gscale, loss, row_a, row_b);
+  return (int)hipGetLastError();
+}
+
+int ast_gram_huber_f32(const float* gx, const float* gy, long long n, float weight, const float* gscale, float* loss,
+                       float* dgram, void* stream) {
+  if (!gx || !gy) return AST_E_NULLPTR;
+  if (n <= 0) return AST_E_SHAPE;
+  hipLaunchKernelGGL(gram_huber_kernel, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, gx, gy,
+                     (int64_t)n, weight, gscale, loss, dgram);
+  return (int)hipGetLastError();
+}
+
+int ast_tv_loss_f32(const float* x, long long planes, int h, int w, float weight, const float* gscale, float* loss,
+                    float* dx, int accumulate, void* stream) {
+  if (!x) return AST_E_NULLPTR;
+  if (planes <= 0 || h <= 0 || w <= 0) return AST_E_SHAPE;
+  hipLaunchKernelGGL(tv_kernel, dim3(grid_for(planes * h * w)), dim3(kThreads), 0, (hipStream_t)stream, x,
+                     (int64_t)planes, h, w, weight, gscale, loss, dx, accumulate ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

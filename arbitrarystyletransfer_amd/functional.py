@@ -1,0 +1,383 @@
+"""Autograd for the HIP ops: torch.autograd.Function wrappers whose forward and backward are
+both HIP kernels of libast_hip.so, so `loss.backward()` in a train.py-style loop runs the
+backward on the GPU through the same C ABI (no PyTorch compute on the path).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from ._lib import HipOpError, check, lib, ptr, stream_ptr
+
+_dev = ops._dev
+
+
+def _s(t):
+    return stream_ptr(t.device)
+
+
+def _empty(shape, like):
+    return torch.empty(shape, device=like.device, dtype=torch.float32)
+
+
+# ------------------------------------------------------------------------------------------------
+# weight packs for the backward (cached per parameter version)
+# ------------------------------------------------------------------------------------------------
+
+class TFPackCache:
+    """Transposed+flipped weight packs (input-gradient filters), refreshed on parameter change."""
+
+    def __init__(self):
+        self._c = {}
+
+    def get(self, weight: torch.Tensor, in_scale=None) -> torch.Tensor:
+        w = _dev(weight.detach(), "weight")
+        key = (weight.data_ptr(), weight._version, ops.WEIGHTS_EPOCH[0],
+               None if in_scale is None else in_scale.data_ptr())
+        hit = self._c.get(id(weight))
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        cout, cin = int(w.shape[0]), int(w.shape[1])
+        out = torch.empty(int(lib().ast_conv3x3_packed_numel(cin, cout)), device=w.device, dtype=torch.float32)
+        check(lib().ast_conv3x3_pack_weights_ex_f32(ptr(w), ptr(out), cout, cin, 1, ptr(in_scale), _s(w)),
+              "pack_weights_ex")
+        self._c[id(weight)] = (key, out)
+        return out
+
+
+_TF = TFPackCache()
+
+
+def conv_input_grad_same(dy, weight, in_scale=None):
+    """Gradient of conv3x3(x, zero pad) wrt x, given dL/dy (same-size transposed conv)."""
+    cout, cin = int(weight.shape[0]), int(weight.shape[1])
+    pre, _, _ = ops.conv3x3(dy, _TF.get(weight, in_scale), None, cin, pad_mode="zeros",
+                            want_pre=True, want_act=False)
+    return pre
+
+
+# id(parameter) -> dp.FlatGradArena: weight gradients are written straight into the arena slice
+# (a fresh view each call, which autograd adopts as .grad without copying).
+GRAD_ARENA = {}
+
+
+def _grad_buffer(param, shape, like):
+    arena = GRAD_ARENA.get(id(param)) if param is not None else None
+    if arena is not None:
+        return arena.view_for(param)
+    return _empty(shape, like)
+
+
+def conv_weight_grad(x, dy, cout, upsample=1, pad_mode="zeros", with_bias=True, weight=None, bias=None):
+    x = _dev(x, "x")
+    dy = _dev(dy, "dy")
+    n, cin, h, w = (int(s) for s in x.shape)
+    dw = _grad_buffer(weight, (cout, cin, 3, 3), x)
+    db = _grad_buffer(bias, (cout,), x) if with_bias else None
+    flops = 2 * n * h * upsample * w * upsample * cout * cin * 9
+    check(ops._timed(f"wgrad {cin}->{cout} {h * upsample}x{w * upsample}", flops, x.device,
+                     lambda: lib().ast_conv3x3_wgrad_f32(ptr(x), ptr(dy), ptr(dw), ptr(db), n, cin, h, w, cout,
+                                                         upsample, ops.PAD_MODES[pad_mode], _s(x))),
+          "conv3x3_wgrad")
+    return dw, db
+
+
+# ------------------------------------------------------------------------------------------------
+# VGG encoder block: conv3x3 (zero pad) -> {pre, ReLU, ReLU+MaxPool} (PretrainedEncoder)
+# ------------------------------------------------------------------------------------------------
+
+class EncoderConvFn(torch.autograd.Function):
+    """Outputs (pre, act, pool) — the conv_i / relu_i / pool_i taps; unrequested ones are empty
+    tensors. `norm` = (mean, std) for conv_1 (Normalization fused into the gather)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, packed, want_act, want_pool, mean, std):
+        ctx.set_materialize_grads(False)
+        pre, act, pool = ops.conv3x3(x, packed, bias, weight.shape[0], pad_mode="zeros", in_mean=mean,
+                                     in_std=std, want_pre=True, want_act=want_act, want_pool=want_pool)
+        ctx.save_for_backward(x, weight, pre, mean, std)
+        ctx.has_bias = bias is not None
+        ctx.param_ids = (weight, bias)
+        e = x.new_empty(0)
+        return pre, (act if act is not None else e), (pool if pool is not None else e)
+
+    @staticmethod
+    def backward(ctx, g_pre, g_act, g_pool):
+        x, weight, pre, mean, std = ctx.saved_tensors
+        n, cout, h, w = pre.shape
+        gp = g_pre if (g_pre is not None and g_pre.numel()) else None
+        ga = g_act if (g_act is not None and g_act.numel()) else None
+        gq = g_pool if (g_pool is not None and g_pool.numel()) else None
+        dy = torch.empty_like(pre)
+        check(lib().ast_conv_act_backward_f32(ptr(pre), ptr(_dev(gp, "g") if gp is not None else None),
+                                              ptr(_dev(ga, "g") if ga is not None else None),
+                                              ptr(_dev(gq, "g") if gq is not None else None), ptr(dy),
+                                              n * cout, h, w, _s(pre)), "conv_act_backward")
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_input_grad_same(dy, weight, std.view(-1) if std is not None else None)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            xin = x
+            if mean is not None:  # conv_1 sees the normalised image
+                xin = normalize_image(x, mean, std)
+            dw, db = conv_weight_grad(xin, dy, cout, with_bias=ctx.has_bias, weight=ctx.param_ids[0],
+                                      bias=ctx.param_ids[1])
+        return dx, dw, db, None, None, None, None, None
+
+
+def normalize_image(x, mean, std):
+    x = _dev(x, "x")
+    n, c = x.shape[:2]
+    out = torch.empty_like(x)
+    m = mean.reshape(-1).repeat(n).contiguous()
+    s = std.reshape(-1).repeat(n).contiguous()
+    check(lib().ast_plane_normalize_f32(ptr(x), ptr(m), ptr(s), ptr(out), n * c, x[0, 0].numel(), _s(x)),
+          "normalize")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Decoder block: [Upsample x2] -> ReflectionPad(1) -> conv3x3 -> [ReLU]
+# ------------------------------------------------------------------------------------------------
+
+class DecoderConvFn(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, packed, upsample, relu):
+        pre, act, _ = ops.conv3x3(x, packed, bias, weight.shape[0], upsample=upsample, pad_mode="reflect",
+                                  want_pre=not relu, want_act=relu)
+        out = act if relu else pre
+        ctx.save_for_backward(x, weight, out)
+        ctx.upsample, ctx.relu, ctx.has_bias = upsample, relu, bias is not None
+        ctx.param_ids = (weight, bias)  # for the DP gradient arena lookup (not saved tensors)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight, out = ctx.saved_tensors
+        g = _dev(g, "grad")
+        n, cout, H, W = out.shape
+        cin = x.shape[1]
+        if ctx.relu:
+            dy = torch.empty_like(g)
+            check(lib().ast_relu_mask_f32(ptr(g), ptr(out), ptr(dy), g.numel(), _s(g)), "relu_mask")
+        else:
+            dy = g
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dpin = conv_input_grad_same(dy, weight)
+            border = torch.empty((n, cin, 2 * (W + 2) + 2 * H), device=g.device, dtype=torch.float32)
+            wdet = _dev(weight.detach(), "weight")
+            check(lib().ast_conv3x3_dgrad_border_f32(ptr(dy), ptr(wdet), ptr(border), n, cout, cin, H, W, _s(g)),
+                  "dgrad_border")
+            dx = torch.empty_like(x)
+            check(lib().ast_pad_up_adjoint_f32(ptr(dpin), ptr(border), None, ptr(dx), n * cin, x.shape[2],
+                                               x.shape[3], ctx.upsample, _s(g)), "pad_up_adjoint")
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dw, db = conv_weight_grad(x, dy, cout, ctx.upsample, "reflect", ctx.has_bias, *ctx.param_ids)
+        return dx, dw, db, None, None, None
+
+
+# ------------------------------------------------------------------------------------------------
+# Statistics / AdaIN
+# ------------------------------------------------------------------------------------------------
+
+class ChannelStatsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, unbiased, eps):
+        mean, std = ops.channel_stats(x, unbiased, eps)
+        ctx.save_for_backward(x, mean, std)
+        ctx.unbiased = unbiased
+        return mean, std
+
+    @staticmethod
+    def backward(ctx, dmean, dstd):
+        x, mean, std = ctx.saved_tensors
+        x = _dev(x, "x")
+        n, c = x.shape[:2]
+        dx = torch.empty_like(x)
+        dm = _dev(dmean, "dmean") if dmean is not None else None
+        ds = _dev(dstd, "dstd") if dstd is not None else None
+        check(lib().ast_channel_stats_backward_f32(ptr(x), ptr(mean), ptr(std), ptr(dm), ptr(ds), ptr(dx), n * c,
+                                                   x[0, 0].numel(), 1 if ctx.unbiased else 0, 0, _s(x)),
+              "channel_stats_backward")
+        return dx, None, None
+
+
+class MeanVarianceNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return ops.mean_variance_norm(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        x = _dev(x, "x")
+        g = _dev(g, "grad")
+        n, c = x.shape[:2]
+        dx = torch.empty_like(x)
+        check(lib().ast_mvn_backward_f32(ptr(x), ptr(g), ptr(dx), n * c, x[0, 0].numel(), 1e-5, _s(x)),
+              "mvn_backward")
+        return dx
+
+
+def channel_stats(x, unbiased=True, eps=0.0):
+    if torch.is_grad_enabled() and x.requires_grad:
+        return ChannelStatsFn.apply(x, unbiased, eps)
+    return ops.channel_stats(x, unbiased, eps)
+
+
+def mean_variance_norm(x):
+    if torch.is_grad_enabled() and x.requires_grad:
+        return MeanVarianceNormFn.apply(x)
+    return ops.mean_variance_norm(x)
+
+
+# ------------------------------------------------------------------------------------------------
+# Losses (scalar outputs; the backward kernels take grad_output as a device scalar)
+# ------------------------------------------------------------------------------------------------
+
+def _scalar(like):
+    return torch.zeros((), device=like.device, dtype=torch.float32)
+
+
+class GramFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, f):
+        f = _dev(f, "tensor")
+        b, c, h, w = f.shape
+        g = _empty((b, c, c), f)
+        check(lib().ast_gram_f32(ptr(f), ptr(g), b, c, h * w, 1.0 / (c * h * w), _s(f)), "gram")
+        ctx.save_for_backward(f)
+        return g
+
+    @staticmethod
+    def backward(ctx, dg):
+        (f,) = ctx.saved_tensors
+        b, c, h, w = f.shape
+        dg = _dev(dg, "grad")
+        df = torch.empty_like(f)
+        check(lib().ast_gram_backward_f32(ptr(f), ptr(dg), ptr(df), None, None, b, c, h * w, 1.0 / (c * h * w),
+                                          None, 0, _s(f)), "gram_backward")
+        return df
+
+
+class HuberFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y):
+        x, y = _dev(x, "input"), _dev(y, "target")
+        if x.shape != y.shape:
+            raise HipOpError(f"huber: shape mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
+        loss = _scalar(x)
+        check(lib().ast_huber_f32(ptr(x), ptr(y), x.numel(), 1.0, None, ptr(loss), None, 0, _s(x)), "huber")
+        ctx.save_for_backward(x, y)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        g = _dev(g, "grad")
+        dx = dy = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            check(lib().ast_huber_f32(ptr(x), ptr(y), x.numel(), 1.0, ptr(g), None, ptr(dx), 0, _s(x)), "huber")
+        if ctx.needs_input_grad[1]:
+            dy = torch.empty_like(y)
+            check(lib().ast_huber_f32(ptr(y), ptr(x), y.numel(), 1.0, ptr(g), None, ptr(dy), 0, _s(y)), "huber")
+        return dx, dy
+
+
+class MVNHuberFn(torch.autograd.Function):
+    """compute_content_loss(mean_variance_norm(x), mean_variance_norm(y)) with y detached (as
+    every call site in train.py), one fused kernel for value and gradient."""
+
+    @staticmethod
+    def forward(ctx, x, y, weight):
+        x, y = _dev(x, "x"), _dev(y, "y")
+        n, c = x.shape[:2]
+        loss = _scalar(x)
+        check(lib().ast_mvn_huber_f32(ptr(x), ptr(y), n * c, x[0, 0].numel(), weight, None, ptr(loss), None, 0,
+                                      _s(x)), "mvn_huber")
+        ctx.save_for_backward(x, y)
+        ctx.weight = weight
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        g = _dev(g, "grad")
+        n, c = x.shape[:2]
+        dx = torch.empty_like(x)
+        check(lib().ast_mvn_huber_f32(ptr(x), ptr(y), n * c, x[0, 0].numel(), ctx.weight, ptr(g), None, ptr(dx), 0,
+                                      _s(x)), "mvn_huber")
+        return dx, None, None
+
+
+class StyleLossFn(torch.autograd.Function):
+    """compute_style_loss(x, y) (losses.py:128-139) with y detached: value in forward; the
+    backward recomputes the statistics and Gram matrices and emits dx in two launches
+    (moment terms fused into the Gram-backward GEMM epilogue)."""
+
+    @staticmethod
+    def forward(ctx, x, y, weight):
+        x, y = _dev(x, "x"), _dev(y, "y")
+        if x.shape[:2] != y.shape[:2]:
+            raise HipOpError("style loss: (N, C) mismatch")
+        loss = _scalar(x)
+        _style_terms(x, y, weight, loss, None, None)
+        ctx.save_for_backward(x, y)
+        ctx.weight = weight
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        _style_terms(x, y, ctx.weight, None, dx, _dev(g, "grad"))
+        return dx, None, None
+
+
+def _style_terms(x, y, weight, loss, dx, gscale, accumulate=False):
+    b, c, h, w = x.shape
+    hw = h * w
+    planes = b * c
+    stats = _empty((planes, 4), x)
+    ra = _empty((planes,), x) if dx is not None else None
+    rb = _empty((planes,), x) if dx is not None else None
+    L = lib()
+    s = _s(x)
+    if y.shape[2:] != x.shape[2:]:
+        raise HipOpError("style loss: feature maps must have the same spatial size")
+    check(L.ast_style_moments_f32(ptr(x), ptr(y), planes, hw, weight, ptr(gscale), ptr(stats), ptr(loss), ptr(ra),
+                                  ptr(rb), s), "style_moments")
+    gx = _empty((b, c, c), x)
+    gy = _empty((b, c, c), x)
+    scale = 1.0 / (c * hw)
+    check(L.ast_gram_f32(ptr(x), ptr(gx), b, c, hw, scale, s), "gram")
+    check(L.ast_gram_f32(ptr(y), ptr(gy), b, c, y[0, 0].numel(), 1.0 / (c * y[0, 0].numel()), s), "gram")
+    dg = _empty((b, c, c), x) if dx is not None else None
+    check(L.ast_gram_huber_f32(ptr(gx), ptr(gy), b * c * c, weight, ptr(gscale), ptr(loss), ptr(dg), s), "gram_huber")
+    if dx is not None:
+        check(L.ast_gram_backward_f32(ptr(x), ptr(dg), ptr(dx), ptr(ra), ptr(rb), b, c, hw, scale, None,
+                                      1 if accumulate else 0, s), "gram_backward")
+
+
+class TVLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img):
+        img = _dev(img, "img")
+        n, c, h, w = img.shape
+        loss = _scalar(img)
+        check(lib().ast_tv_loss_f32(ptr(img), n * c, h, w, 1.0, None, ptr(loss), None, 0, _s(img)), "tv_loss")
+        ctx.save_for_backward(img)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (img,) = ctx.saved_tensors
+        n, c, h, w = img.shape
+        dx = torch.empty_like(img)
+        check(lib().ast_tv_loss_f32(ptr(img), n * c, h, w, 1.0, ptr(_dev(g, "grad")), None, ptr(dx), 0, _s(img)),
+              "tv_loss")
+        return dx

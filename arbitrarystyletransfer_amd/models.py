@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F  # noqa: F401  (re-exported like the reference)
 
+from . import functional as Fn
 from . import ops, synth
 from .conf import *  # noqa: F401,F403
 from .conf import device  # noqa: F401
@@ -38,6 +39,9 @@ class AdaIN(nn.Module):
         self.canonical = canonical
 
     def forward(self, content_map, style_map, alpha: float = 1.0):
+        if torch.is_grad_enabled() and (content_map.requires_grad or style_map.requires_grad):
+            raise NotImplementedError("AdaIN backward is not implemented on HIP yet; the AdaIN training step "
+                                      "trains the decoder only (encode under torch.no_grad())")
         return ops.adain(content_map, style_map, alpha=alpha, swap_style_stats=not self.canonical)
 
 
@@ -45,12 +49,16 @@ def calc_mean_std(feat, eps=1e-5):
     """models.py:54-62: per-(n,c) mean and sqrt(unbiased var + eps)."""
     if feat.dim() != 4:
         raise AssertionError("calc_mean_std expects a 4-D tensor")  # models.py:57
-    return ops.channel_stats(feat, unbiased=True, eps=eps)
+    return Fn.channel_stats(feat, unbiased=True, eps=eps)
 
 
 def mean_variance_norm(feat):
     """models.py:64-68."""
-    return ops.mean_variance_norm(feat)
+    return Fn.mean_variance_norm(feat)
+
+
+def _needs_grad(x, module):
+    return torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in module.parameters()))
 
 
 class Normalization(nn.Module):
@@ -87,7 +95,7 @@ class _PackedConvCache:
     def get(self, conv: nn.Conv2d) -> torch.Tensor:
         w = conv.weight
         key = id(conv)
-        stamp = (w.data_ptr(), w._version, w.device)
+        stamp = (w.data_ptr(), w._version, w.device, ops.WEIGHTS_EPOCH[0])
         hit = self._cache.get(key)
         if hit is not None and hit[0] == stamp:
             return hit[1]
@@ -172,6 +180,10 @@ class PretrainedEncoder(nn.Module):
         """Feature maps of the requested layers. `x2` (optional, same C/H/W): a second batch
         encoded in the same launches, outputs hold x's images then x2's."""
         norm = self._vgg_layers[0]
+        if _needs_grad(x, self) or (x2 is not None and _needs_grad(x2, self)):
+            if x2 is not None:
+                return [torch.cat(p) for p in zip(self._forward_autograd(x), self._forward_autograd(x2))]
+            return self._forward_autograd(x)
         outs = []
         cur, cur2 = x, x2
         for idx, conv, want_pre, want_act, want_pool, collect in self._plan():
@@ -183,6 +195,22 @@ class PretrainedEncoder(nn.Module):
             by_name = {conv.name: pre, f"relu_{idx}": act, f"pool_{idx}": pool}
             outs.extend(by_name[nm] for nm in collect)
             cur, cur2 = (pool if want_pool else act), None
+        return outs
+
+    def _forward_autograd(self, x):
+        """Same walk through EncoderConvFn (HIP forward + HIP backward; the pre-ReLU output is
+        always kept for the ReLU / max-pool backward)."""
+        norm = self._vgg_layers[0]
+        outs = []
+        cur = x
+        for idx, conv, want_pre, want_act, want_pool, collect in self._plan():
+            first = idx == 1
+            pre, act, pool = Fn.EncoderConvFn.apply(
+                cur, conv.weight, conv.bias, self._packed.get(conv), want_act, want_pool,
+                norm.mean.view(-1) if first else None, norm.std.view(-1) if first else None)
+            by_name = {conv.name: pre, f"relu_{idx}": act, f"pool_{idx}": pool}
+            outs.extend(by_name[nm] for nm in collect)
+            cur = pool if want_pool else act
         return outs
 
 
@@ -228,6 +256,10 @@ class VGGDecoder(nn.Sequential):
             conv.bias.copy_(torch.from_numpy(b))
 
     def forward(self, x):
+        if _needs_grad(x, self):
+            for conv, up, relu in self._groups:
+                x = Fn.DecoderConvFn.apply(x, conv.weight, conv.bias, self._packed.get(conv), 2 if up else 1, relu)
+            return x
         for conv, up, relu in self._groups:
             pre, act, _ = ops.conv3x3(x, self._packed.get(conv), conv.bias, conv.out_channels,
                                       upsample=2 if up else 1, pad_mode="reflect",

@@ -13,6 +13,14 @@ from ._lib import HipOpError, check, lib, ptr, stream_ptr
 
 PAD_MODES = {"zeros": 0, "reflect": 1}
 
+# Bumped by optimizers that update parameters through raw pointers (optim.FusedAdam), which
+# torch's per-tensor _version counter cannot see; weight-pack caches key on it.
+WEIGHTS_EPOCH = [0]
+
+
+def bump_weights_epoch():
+    WEIGHTS_EPOCH[0] += 1
+
 
 class LaunchTimer:
     """Records a pair of HIP events around every conv3x3 launch, on the launch stream, while

@@ -1,0 +1,135 @@
+"""Optimizer step of train.py:287-300 on HIP: clip_grad_norm_(params, max_norm,
+error_if_nonfinite) + torch.optim.Adam, as two multi-tensor launches (optim.hip).
+
+FusedAdam keeps torch.optim.Adam's param_groups/state layout ('step', 'exp_avg', 'exp_avg_sq'),
+so `ast_optim` state dicts interchange with the reference's checkpoints (train.py:103-115).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import ops
+from ._lib import check, lib, ptr, stream_ptr
+
+
+class _Table:
+    """Device copy of the (param, grad, exp_avg, exp_avg_sq, numel) table, staged through a
+    pinned host buffer (one small H2D copy on the stream, no host sync in steady state)."""
+
+    def __init__(self):
+        self.host = None
+        self.dev = None
+        self.event = None
+
+    def build(self, params, grads, ms, vs, device):
+        L = lib()
+        n = len(params)
+        nbytes = int(L.ast_optim_table_bytes(n))
+        if self.host is None or self.host.numel() < nbytes:
+            self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+            self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        if self.event is not None:
+            self.event.synchronize()  # previous copy out of the pinned buffer has finished
+        arr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() if t is not None else 0 for t in ts])  # noqa: E731
+        numel = (ctypes.c_longlong * n)(*[t.numel() for t in params])
+        nchunks = L.ast_optim_build_table(ctypes.c_void_p(self.host.data_ptr()), n, arr(params), arr(grads),
+                                          arr(ms) if ms is not None else None,
+                                          arr(vs) if vs is not None else None, numel)
+        if nchunks < 0:
+            raise RuntimeError("optimizer table: null tensor")
+        self.dev[:nbytes].copy_(self.host[:nbytes], non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record(torch.cuda.current_stream(device))
+        return nchunks
+
+
+def _grad_norm_state(table, n, nchunks, max_norm, device):
+    partial = torch.empty(nchunks, device=device, dtype=torch.float32)
+    state = torch.empty(2, device=device, dtype=torch.float32)
+    check(lib().ast_grad_norm_f32(ptr(table.dev), n, nchunks, ptr(partial), float(max_norm), ptr(state),
+                                  stream_ptr(device)), "grad_norm")
+    return state
+
+
+def _check_finite(norm):
+    v = float(norm.item())
+    if v != v or v in (float("inf"), float("-inf")):
+        raise RuntimeError(f"The total norm of order 2.0 for gradients from `parameters` is non-finite ({v}), "
+                           "so it cannot be clipped (error_if_nonfinite=True, train.py:292)")
+
+
+class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam (amsgrad off, no weight decay) with an optional fused
+    clip_grad_norm_(max_grad_norm, error_if_nonfinite) in front, all on HIP."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 max_grad_norm=None, error_if_nonfinite=False):
+        if weight_decay != 0.0:
+            raise ValueError("FusedAdam: weight_decay is not supported (the reference uses 0)")
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=0.0, amsgrad=False, maximize=False,
+                        foreach=None, capturable=False, differentiable=False, fused=None)
+        super().__init__(params, defaults)
+        self.max_grad_norm = max_grad_norm
+        self.error_if_nonfinite = error_if_nonfinite
+        self._tables = {}
+        self.last_grad_norm = None
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            dev = params[0].device
+            for p in params:
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+            grads = [ops._dev(p.grad, "grad") for p in params]
+            table = self._tables.setdefault(gi, _Table())
+            nchunks = table.build([p.data for p in params], grads, [self.state[p]["exp_avg"] for p in params],
+                                  [self.state[p]["exp_avg_sq"] for p in params], dev)
+            state = None
+            if self.max_grad_norm is not None:
+                state = _grad_norm_state(table, len(params), nchunks, self.max_grad_norm, dev)
+                self.last_grad_norm = state[0]
+                if self.error_if_nonfinite:
+                    _check_finite(state[0])
+            step = int(self.state[params[0]]["step"].item())
+            b1, b2 = group["betas"]
+            check(lib().ast_adam_step_f32(ptr(table.dev), len(params), nchunks, ptr(state), float(group["lr"]),
+                                          float(b1), float(b2), float(group["eps"]), step, stream_ptr(dev)),
+                  "adam_step")
+        ops.bump_weights_epoch()
+        return loss
+
+
+def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=False):
+    """torch.nn.utils.clip_grad_norm_ for L2 on HIP: returns the total norm (device scalar) and
+    scales the gradients in place by min(1, max_norm / (norm + 1e-6))."""
+    if norm_type != 2.0:
+        raise ValueError("only the L2 norm is implemented")
+    if isinstance(parameters, torch.Tensor):
+        parameters = [parameters]
+    params = [p for p in parameters if p.grad is not None]
+    if not params:
+        return torch.tensor(0.0)
+    dev = params[0].device
+    table = _Table()
+    grads = [ops._dev(p.grad, "grad") for p in params]
+    nchunks = table.build(grads, grads, None, None, dev)
+    state = _grad_norm_state(table, len(params), nchunks, max_norm, dev)
+    if error_if_nonfinite:
+        _check_finite(state[0])
+    # scale: an Adam step with lr 0 would also touch moments; use the scale-only path instead
+    check(lib().ast_grad_scale_f32(ptr(table.dev), len(params), nchunks, ptr(state), stream_ptr(dev)), "grad_scale")
+    return state[0]

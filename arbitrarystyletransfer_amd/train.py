@@ -1,0 +1,112 @@
+"""AdaIN training step on HIP: the counterpart of the reference's ASTTrainer (train.py:50-401)
+for the VGG AdaIN network (BASELINE.json configs 3-4).
+
+Per step (train.py:191-300, AdaIN version):
+  stylised = decoder(AdaIN(enc(content), enc(style)))            (encoder frozen, under no_grad)
+  content_map, style_map, t_cs_map = lossnet(content|style|stylised)   (VGG19 to relu_15)
+  content = sum_i huber(mvn(t_cs_map[i]), mvn(content_map[i])) + 0.1 * pixel term     (:217-227, :258)
+  style   = sum_i w_i * style_loss(t_cs_map[i], style_map[i]) + style_loss(stylised, style)  (:230-245, :271)
+            w = 1, 1, 1, 1, 0.75, 0.5
+  lf      = huber(mvn(t), mvn(enc(stylised).detach()))           (:276-277; no gradient: t is constant)
+  tv      = tv_loss(stylised)                                      (:282)
+  loss    = 1.25*content + 0.5*style + 1.0*lf + 6e-4*tv            (:283, defaults :416-425)
+  Adam(lr 2e-4, betas (0.9, 0.999), eps 1e-5) after clip_grad_norm_(2.0, error_if_nonfinite).
+The hist / org_img / out_of_range terms of train.py:255-269 belong to the AdaAttN model and the
+histogram loss (SURVEY.md §8f "next") and are not part of this step.
+
+Data parallel (config 4): one process per GPU, each with its own batch shard; decoder gradients
+land in one flat buffer and are averaged with a single all-reduce (RCCL over xGMI) before the
+optimizer step (dp.py).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+
+import torch
+
+from . import losses as L
+from . import models
+from .optim import FusedAdam
+
+STYLE_WEIGHTS = (1.0, 1.0, 1.0, 1.0, 0.75, 0.5)   # train.py:232-238 for the 6 loss-network layers
+
+
+def default_args(**kw):
+    a = dict(train_iter=10, batch_size=8, lr=2e-4, content_lam=1.25, style_lam=0.5, tv_lam=0.0006, lf_lam=1.0,
+             save_dir="models/ast/", load=False, image_size=512)
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+class AdaINTrainer:
+    def __init__(self, args=None, device=None, net=None, lossnet=None, grad_hook=None):
+        self.args = args or default_args()
+        self.device = torch.device(device or "cuda")
+        self.net = (net or models.AdaINStyleTransfer()).to(self.device)
+        self.net.encoder.requires_grad_(False).eval()
+        self.lossnet = (lossnet or models.PretrainedEncoder()).to(self.device).eval()
+        self.lossnet.requires_grad_(False)
+        self.params = [p for p in self.net.decoder.parameters()]
+        self.optim = FusedAdam(self.params, lr=self.args.lr, betas=(0.9, 0.999), eps=1e-5, max_grad_norm=2.0,
+                               error_if_nonfinite=True)
+        self.grad_hook = grad_hook  # called between backward and the optimizer step (DP all-reduce)
+        self.train_dict = {"content_loss": [], "style_loss": [], "lf_loss": [], "tv_loss": [], "org_img_loss": []}
+        self.save_file = os.path.join(self.args.save_dir, "ast.pth")
+        self.train_dict_file = os.path.join(self.args.save_dir, "ast_train_dict.json")
+
+    # ---- one step ----------------------------------------------------------------------------
+    def compute_losses(self, content, style):
+        a = self.args
+        with torch.no_grad():
+            f_c, f_s = self.net.encode_pair(content, style)
+            t = self.net.adain(f_c, f_s)
+            content_map = self.lossnet(content, style)          # both batches in the same launches
+            b = content.shape[0]
+            style_map = [m[b:] for m in content_map]
+            content_map = [m[:b] for m in content_map]
+        stylized = self.net.decoder(t)
+        t_cs_map = self.lossnet(stylized)
+        with torch.no_grad():
+            enc_stylized = self.net.encoder(stylized.detach())[0]
+            lf_loss = L.content_mvn_loss(t, enc_stylized)
+
+        content_terms = [L.content_mvn_loss(t_cs_map[i], content_map[i]) for i in range(len(t_cs_map))]
+        content_terms.append(L.content_mvn_loss(stylized, content, 0.1))
+        style_terms = [L.style_loss_weighted(t_cs_map[i], style_map[i], STYLE_WEIGHTS[i]) for i in range(len(t_cs_map))]
+        style_terms.append(L.style_loss_weighted(stylized, style, 1.0))
+        tv = L.tv_loss(stylized)
+        content_loss = torch.stack(content_terms).sum()
+        style_loss = torch.stack(style_terms).sum()
+        loss = a.content_lam * content_loss + a.style_lam * style_loss + a.lf_lam * lf_loss + a.tv_lam * tv
+        return {"loss": loss, "content_loss": content_loss, "style_loss": style_loss, "lf_loss": lf_loss,
+                "tv_loss": tv, "stylized": stylized}
+
+    def train_step(self, content, style, record=False):
+        out = self.compute_losses(content, style)
+        self.optim.zero_grad(set_to_none=True)
+        out["loss"].backward()
+        if self.grad_hook is not None:
+            self.grad_hook(self.params)
+        self.optim.step()
+        out["grad_norm"] = self.optim.last_grad_norm
+        if record:  # device -> host syncs, as train.py:302-306 does every step
+            for k in ("content_loss", "style_loss", "lf_loss", "tv_loss"):
+                self.train_dict[k].append(float(out[k].item()))
+            self.train_dict["org_img_loss"].append(0.0)
+        return out
+
+    # ---- checkpoints (train.py:103-133) -------------------------------------------------------
+    def save(self):
+        os.makedirs(self.args.save_dir, exist_ok=True)
+        torch.save({"ast": self.net.state_dict(), "ast_optim": self.optim.state_dict()}, self.save_file)
+        with open(self.train_dict_file, "w") as f:
+            json.dump(self.train_dict, f)
+
+    def load(self):
+        d = torch.load(self.save_file, map_location=self.device, weights_only=True)
+        self.net.load_state_dict(d["ast"])
+        self.optim.load_state_dict(d["ast_optim"])
+        with open(self.train_dict_file) as f:
+            self.train_dict = json.load(f)

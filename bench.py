@@ -45,7 +45,67 @@ def parse():
     p.add_argument("--size", type=int, default=512)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(os.cpu_count(), OMP_NUM_THREADS or 16)")
+    p.add_argument("--mode", choices=["fwd", "train"], default="fwd",
+                   help="fwd: config 2 (the headline metric); train: config 3/4 AdaIN training step")
     return p.parse_args()
+
+
+def train_bench(args, dev, rank, world):
+    """Config 3 (bs=16, 1 GPU) / config 4 (bs=8 per GPU, RCCL gradient all-reduce): one step =
+    forward, loss network x3, losses, backward, all-reduce (N>1), clip + Adam."""
+    from arbitrarystyletransfer_amd import dp
+    from arbitrarystyletransfer_amd.train import AdaINTrainer, default_args
+    B, S = args.batch, args.size
+    arena = None
+    trainer = AdaINTrainer(default_args(batch_size=B, image_size=S), device=dev)
+    if world > 1:
+        arena = dp.FlatGradArena(trainer.params)
+        trainer.grad_hook = arena
+    content = torch.from_numpy(synth.image(777 + 2 * rank, (B, 3, S, S))).to(dev)
+    style = torch.from_numpy(synth.image(778 + 2 * rank, (B, 3, S, S))).to(dev)
+    for _ in range(args.warmup):
+        trainer.train_step(content, style)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    timer = ops.LaunchTimer()
+    t0 = time.perf_counter()
+    with timer:
+        for _ in range(args.steps):
+            out = trainer.train_step(content, style)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out["loss"]), "non-finite loss"
+    recs = timer.results()
+    mm = [(tag, fl, ms) for tag, fl, ms in recs if tag.startswith(("conv3x3", "wgrad"))]
+    fl = sum(f for _, f, _ in mm)
+    ms = sum(m for _, _, m in mm)
+    tf = fl / (ms * 1e-3) / 1e12
+    wg = [(f, m) for tag, f, m in mm if tag.startswith("wgrad")]
+    wg_tf = sum(f for f, _ in wg) / (sum(m for _, m in wg) * 1e-3) / 1e12 if wg else None
+    result = {
+        "metric": "AdaIN training images/sec at 512x512 (config 3: bs=16/GPU; config 4: batch-sharded)",
+        "value": B * world * args.steps / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (live-init weights, U[0,1) images), resident in HBM",
+        "config": {"workload": f"AdaIN train step (decoder trained; VGG loss network to relu_15; content+style+"
+                               f"lf+tv losses; clip 2.0 + Adam), bs={B}/GPU {S}x{S} fp32",
+                   "global_batch": B * world, "image_size": S, "parallelism": f"data-parallel x{world}"},
+        "roofline": {"bound": "mfma", "kernel": "conv3x3 fwd/dgrad + wgrad MFMA launches of a step",
+                     "achieved": tf, "peak": PEAK_FP32_MFMA_TF, "unit": "TFLOP/s", "frac": tf / PEAK_FP32_MFMA_TF,
+                     "traffic": None, "wgrad_tflops": wg_tf,
+                     "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3),
+                     "mfma_tflop_per_step": fl / args.steps / 1e12},
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
 
 
 def cpu_baseline(size, seconds, threads):
@@ -92,6 +152,11 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    if args.mode == "train":
+        train_bench(args, dev, rank, world)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     B, S = args.batch, args.size
     net = models.AdaINStyleTransfer().to(dev).eval()

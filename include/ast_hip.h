@@ -94,6 +94,127 @@ int ast_adain_f32(const float* content, const float* style, float* out,
 int ast_plane_normalize_f32(const float* x, const float* mean, const float* std, float* out,
                             long long planes, long long hw, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * 3x3 conv backward (training step). Input gradients run ast_conv3x3_fwd_f32_cfg on a
+ * transposed+flipped pack of the filter (cin' = cout, cout' = cin, zero padding):
+ * dgrad_same(dy) = gradient of the padded input at its interior.
+ * ------------------------------------------------------------------------------------------ */
+
+/* transpose_flip = 0: same as ast_conv3x3_pack_weights_f32. transpose_flip = 1: pack
+ * W'[ci][co][ky][kx] = W[co][ci][2-ky][2-kx] / (in_scale ? in_scale[ci] : 1) (in_scale folds
+ * the conv_1 normalisation's 1/std into the image gradient); its packed size is
+ * ast_conv3x3_packed_numel(cin, cout). */
+int ast_conv3x3_pack_weights_ex_f32(const float* w, float* w_packed, int cout, int cin,
+                                    int transpose_flip, const float* in_scale, void* stream);
+
+/* Backward of y_pre -> ReLU -> [MaxPool2d(2,2)] (models.py:216-218):
+ * dy = g_pre + (pre > 0) * (g_act + unpool(g_pool)); any of g_pre/g_act/g_pool may be NULL.
+ * pre [planes, h, w], g_pool [planes, h/2, w/2]. */
+int ast_conv_act_backward_f32(const float* pre, const float* g_pre, const float* g_act,
+                              const float* g_pool, float* dy, long long planes, int h, int w,
+                              void* stream);
+
+/* out = mask > 0 ? g : 0 (ReLU backward given the ReLU output). */
+int ast_relu_mask_f32(const float* g, const float* mask, float* out, long long n, void* stream);
+
+/* Reflect-pad dgrad border: gradient of the padded input on padded rows 0, h+1 and columns
+ * 0, w+1 (dy [n, cout, h, w], w [cout, cin, 3, 3] unpacked); border [n, cin, 2(w+2)+2h]. */
+int ast_conv3x3_dgrad_border_f32(const float* dy, const float* w, float* border,
+                                 int n, int cout, int cin, int h, int w_, void* stream);
+
+/* Adjoint of Upsample(x upsample, nearest) -> ReflectionPad2d(1): folds the padded-input
+ * gradient (interior dp_interior [planes, h_in*up, w_in*up] + border) onto the source grid
+ * dx [planes, h_in, w_in]; mask (optional, = the ReLU output that fed the layer): dx *= mask>0. */
+int ast_pad_up_adjoint_f32(const float* dp_interior, const float* border, const float* mask,
+                           float* dx, long long planes, int h_in, int w_in, int upsample,
+                           void* stream);
+
+/* dw [cout, cin, 3, 3] = sum over images/pixels of dy x pad(upsample(x)) (zeroed here, MFMA
+ * fp32, split over pixel tiles with fp32 atomics); db [cout] = sum of dy (optional). */
+int ast_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, float* db,
+                          int n, int cin, int h_in, int w_in, int cout,
+                          int upsample, int pad_mode, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Losses (losses.py). Loss values are ADDED into the device scalar `loss` (may be NULL);
+ * gradients are written (accumulate=0) or added (accumulate=1) into `dx` (may be NULL = value
+ * only). `weight` multiplies both; `gscale` (device scalar or NULL) multiplies the gradient only
+ * (autograd's grad_output).
+ * ------------------------------------------------------------------------------------------ */
+
+/* gram_matrix (losses.py:105-109): gram[b] = scale * feat[b] feat[b]^T, feat [n, c, hw],
+ * gram [n, c, c] (zeroed here; split-K MFMA with fp32 atomics). */
+int ast_gram_f32(const float* feat, float* gram, int n, int c, long long hw, float scale, void* stream);
+
+/* dfeat[b] (+)= scale * (dgram[b] + dgram[b]^T) feat[b] + row_a[b,i] * feat[b,i,:] + row_b[b,i]
+ * (the backward of gram_matrix, with compute_style_loss's mean/std gradients fused: row_a/row_b
+ * from ast_style_moments_f32, or both NULL). */
+int ast_gram_backward_f32(const float* feat, const float* dgram, float* dfeat,
+                          const float* row_a, const float* row_b,
+                          int n, int c, long long hw, float scale, const float* gscale,
+                          int accumulate, void* stream);
+
+/* compute_content_loss(mean_variance_norm(x), mean_variance_norm(y)) (losses.py:124-126,
+ * models.py:64-68; train.py:225): loss += weight * mean(huber(mvn(x) - mvn(y))), dx = d/dx. */
+int ast_mvn_huber_f32(const float* x, const float* y, long long planes, long long hw, float weight,
+                      const float* gscale, float* loss, float* dx, int accumulate, void* stream);
+
+/* compute_content_loss(x, y) = F.huber_loss(x, y) (delta 1, mean). */
+int ast_huber_f32(const float* x, const float* y, long long n, float weight, const float* gscale,
+                  float* loss, float* dx, int accumulate, void* stream);
+
+/* Mean/std part of compute_style_loss (losses.py:130-134):
+ * loss += weight * 1.25 * (mean huber(mu_x - mu_y) + mean huber(sd_x - sd_y)) over planes,
+ * stats [planes, 4] = (mu_x, sd_x, mu_y, sd_y); row_a/row_b [planes] = per-plane gradient
+ * d/dx = row_a * x + row_b (NULL: value only). */
+int ast_style_moments_f32(const float* x, const float* y, long long planes, long long hw, float weight,
+                          const float* gscale, float* stats, float* loss, float* row_a, float* row_b,
+                          void* stream);
+
+/* Gram part of compute_style_loss (losses.py:135-137): loss += weight * 10 * mean(huber(gx-gy)),
+ * dgram = d/dgx (NULL: value only). */
+int ast_gram_huber_f32(const float* gx, const float* gy, long long n, float weight, const float* gscale,
+                       float* loss, float* dgram, void* stream);
+
+/* tv_loss (losses.py:90-103): loss += weight * tv(x); dx (+)= d/dx. x [planes, h, w]. */
+int ast_tv_loss_f32(const float* x, long long planes, int h, int w, float weight, const float* gscale,
+                    float* loss, float* dx, int accumulate, void* stream);
+
+/* Backward of mean_variance_norm (models.py:64-68) given the output gradient g. */
+int ast_mvn_backward_f32(const float* x, const float* g, float* dx, long long planes, long long hw,
+                         float eps, void* stream);
+
+/* Backward of channel_stats / calc_mean_std: dx (+)= dmean/N + dstd*(x-mean)/((N-unbiased)*std);
+ * dmean or dstd may be NULL. */
+int ast_channel_stats_backward_f32(const float* x, const float* mean, const float* std,
+                                   const float* dmean, const float* dstd, float* dx,
+                                   long long planes, long long hw, int unbiased, int accumulate,
+                                   void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Optimizer (train.py:287-300): clip_grad_norm_ + torch.optim.Adam over many tensors in two
+ * launches. The caller builds a tensor table on the host (ast_optim_build_table, returns the
+ * number of 64K-element chunks = workgroups), copies it to device memory once, and reuses it.
+ * ------------------------------------------------------------------------------------------ */
+size_t ast_optim_table_bytes(int ntensors);
+long long ast_optim_build_table(void* host_table, int ntensors, float* const* params,
+                                float* const* grads, float* const* exp_avg,
+                                float* const* exp_avg_sq, const long long* numel);
+
+/* state[0] = sqrt(sum of squared grads), state[1] = min(1, max_norm/(state[0]+1e-6))
+ * (max_norm <= 0: coefficient 1). partial: nchunks floats of scratch. */
+int ast_grad_norm_f32(const void* dev_table, int ntensors, long long nchunks, float* partial,
+                      float max_norm, float* state, void* stream);
+
+/* grads *= state[1] (the clip_grad_norm_ scaling alone). */
+int ast_grad_scale_f32(const void* dev_table, int ntensors, long long nchunks, const float* state,
+                       void* stream);
+
+/* grads *= state[1] (if state) then one Adam step (step = 1-based count; lr, betas, eps as in
+ * torch.optim.Adam, amsgrad off, no weight decay). */
+int ast_adam_step_f32(const void* dev_table, int ntensors, long long nchunks, const float* state,
+                      double lr, double beta1, double beta2, double eps, int step, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -189,7 +189,64 @@ def main():
                         gram_grad=gram_grad.numpy(), style_loss=sl.detach().numpy(), style_grad=style_grad.numpy(),
                         content_loss=cl.detach().numpy(), content_grad=content_grad.numpy(),
                         img=img.detach().numpy(), tv=tv.detach().numpy(), tv_grad=img.grad.numpy())
+    train_step_golden(R, enc_wb, dec_wb)
     print("golden vectors written to", HERE)
+
+
+def train_step_golden(R, enc_wb, dec_wb):
+    """One AdaIN training step assembled from the reference's own functions
+    exactly as train.py:191-300 assembles its losses: lifted PretrainedEncoder / AdaIN /
+    mean_variance_norm, the commented decoder spec, losses.py, torch Adam + clip_grad_norm_."""
+    import copy
+    L = R["_losses"]
+    mvn = R["mean_variance_norm"]
+    torch.manual_seed(0)
+    enc = R["PretrainedEncoder"](content_layers=["relu_9"]).eval()
+    set_convs(enc, enc_wb)
+    lossnet = R["PretrainedEncoder"]().eval()
+    set_convs(lossnet, enc_wb)
+    for p in list(enc.parameters()) + list(lossnet.parameters()):
+        p.requires_grad_(False)
+    dec = copy.deepcopy(R["decoder"]).train()
+    set_convs(dec, dec_wb)
+    adain = R["AdaIN"]()
+    opt = torch.optim.Adam(dec.parameters(), lr=2e-4, betas=[0.9, 0.999], eps=1e-5)   # train.py:61
+    content = torch.from_numpy(synth.image(811, (2, 3, 64, 64)))
+    style = torch.from_numpy(synth.image(812, (2, 3, 64, 64)))
+
+    with torch.no_grad():
+        t = adain(enc(content)[0], enc(style)[0])
+    stylized = dec(t)
+    content_map = lossnet(content)
+    style_map = lossnet(style)
+    t_cs_map = lossnet(stylized)
+    enc_stylized = enc(stylized)
+    for i in range(len(t_cs_map)):                                                     # train.py:217-227
+        term = L.compute_content_loss(mvn(t_cs_map[i]), mvn(content_map[i].detach())) * 1.0
+        content_loss = term if i == 0 else content_loss + term
+    for i in range(len(t_cs_map)):                                                     # train.py:230-245
+        w = 0.5 if i == len(t_cs_map) - 1 else (0.75 if i == len(t_cs_map) - 2 else 1.0)
+        term = L.compute_style_loss(t_cs_map[i], style_map[i].detach()) * w
+        style_loss = term if i == 0 else style_loss + term
+    content_loss = content_loss + L.compute_content_loss(mvn(stylized), mvn(content)) * 0.1   # :258
+    style_loss = style_loss + L.compute_style_loss(stylized, style) * 1.0                     # :271
+    lf_loss = L.compute_content_loss(mvn(t), mvn(enc_stylized[0].detach()))                  # :276-277
+    tv = L.tv_loss(stylized)                                                                 # :282
+    loss = 1.25 * content_loss + 0.5 * style_loss + 1.0 * lf_loss + 0.0006 * tv             # :283
+    opt.zero_grad()
+    loss.backward()
+    grads = [p.grad.detach().clone() for p in dec.parameters()]
+    norm = torch.nn.utils.clip_grad_norm_(dec.parameters(), 2.0, error_if_nonfinite=True)  # :292
+    opt.step()
+    out = dict(content=content.numpy(), style=style.numpy(), stylized=stylized.detach().numpy(),
+               content_loss=content_loss.detach().numpy(), style_loss=style_loss.detach().numpy(),
+               lf_loss=lf_loss.detach().numpy(), tv_loss=tv.detach().numpy(), loss=loss.detach().numpy(),
+               grad_norm=norm.detach().numpy())
+    for i, (g, p) in enumerate(zip(grads, dec.parameters())):
+        out[f"grad{i}"] = g.numpy() if g.numel() <= 4096 else g.reshape(-1)[::97].numpy()
+        out[f"grad{i}_sum"] = np.array([g.double().sum().item(), g.double().abs().sum().item()])
+        out[f"param{i}"] = p.detach().numpy() if p.numel() <= 4096 else p.detach().reshape(-1)[::97].numpy()
+    np.savez_compressed(os.path.join(HERE, "train_step_64.npz"), **out)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,72 @@
+"""CPU (gloo, world size 2): the data-parallel logic of dp.py — batch sharding, the flat
+gradient arena and its all-reduce — driven with real decoder gradients from the CPU oracle's
+AdaIN training losses. The DP step must equal the single-process step on the mean of the
+per-shard losses (the DDP semantics used for BASELINE.json config 4)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from arbitrarystyletransfer_amd import dp, synth
+
+
+def test_shard_range():
+    assert [dp.shard_range(64, r, 8) for r in range(8)] == [(8 * r, 8 * r + 8) for r in range(8)]
+    spans = [dp.shard_range(10, r, 4) for r in range(4)]
+    assert spans == [(0, 3), (3, 6), (6, 8), (8, 10)]
+    assert [dp.shard_range(3, r, 4) for r in range(4)] == [(0, 1), (1, 2), (2, 3), (3, 3)]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _grads_for(content, style, lr_params):
+    from oracle import ref_cpu as R
+    enc = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_encoder_weights(1)]
+    dec = [(w.clone().requires_grad_(), b.clone().requires_grad_()) for w, b in lr_params]
+    out = R.train_losses(content, style, enc, dec)
+    out["loss"].backward()
+    return [t.grad for wb in dec for t in wb], float(out["loss"])
+
+
+def _worker(rank, world, port, content, style, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    dec_wb = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_decoder_weights(2)]
+    a, b = dp.shard_range(content.shape[0], rank, world)
+    grads, loss = _grads_for(content[a:b], style[a:b], dec_wb)
+    params = [torch.nn.Parameter(t.clone()) for wb in dec_wb for t in wb]
+    for p, g in zip(params, grads):
+        p.grad = g
+    arena = dp.FlatGradArena(params, device=torch.device("cpu"))
+    try:
+        arena.all_reduce()
+    finally:
+        arena.unregister()
+    if rank == 0:
+        torch.save({"flat": arena.flat.clone(), "loss": loss}, result_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_gradient_average_matches_single_process(tmp_path):
+    content = torch.from_numpy(synth.image(901, (4, 3, 16, 16)))
+    style = torch.from_numpy(synth.image(902, (4, 3, 16, 16)))
+    path = str(tmp_path / "r0.pt")
+    mp.spawn(_worker, args=(2, _free_port(), content, style, path), nprocs=2, join=True)
+    got = torch.load(path, weights_only=True)["flat"]
+    dec_wb = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_decoder_weights(2)]
+    g0, _ = _grads_for(content[:2], style[:2], dec_wb)
+    g1, _ = _grads_for(content[2:], style[2:], dec_wb)
+    ref = torch.cat([((x + y) / 2).reshape(-1) for x, y in zip(g0, g1)])
+    np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-5, atol=1e-7 * float(ref.abs().max()))

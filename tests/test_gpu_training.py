@@ -1,0 +1,247 @@
+"""GPU parity of the training path: every backward kernel against CPU
+autograd of the oracle's ops on the same inputs, the loss kernels against the reference's golden
+values/gradients, FusedAdam against torch.optim.Adam, and one full AdaIN training step against
+the golden step produced by the reference's own functions (tests/golden/train_step_64.npz).
+
+Tolerances: single ops rel_inf <= 5e-5 (fp32, different summation order; wgrad sums up to 10^5
+products); the full step: loss terms rtol 1e-4, gradient sums rtol 2e-3, updated params atol 2e-6.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from arbitrarystyletransfer_amd import functional as Fn
+from arbitrarystyletransfer_amd import losses as L
+from arbitrarystyletransfer_amd import models, optim, synth
+from oracle import ref_cpu as R
+
+pytestmark = pytest.mark.gpu
+TOL = 5e-5
+
+
+def rel_inf(a, b):
+    a = np.asarray(a.detach().cpu() if torch.is_tensor(a) else a, np.float64)
+    b = np.asarray(b.detach().cpu() if torch.is_tensor(b) else b, np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def rnd(seed, shape, scale=1.0, shift=0.0):
+    return torch.from_numpy((synth.uniform(seed, int(np.prod(shape))) * scale + shift).astype(np.float32).reshape(shape))
+
+
+ENC_CASES = [
+    # n, cin, h, w, cout, act, pool, first
+    (2, 3, 16, 40, 64, True, False, True),
+    (1, 16, 16, 32, 64, False, True, False),
+    (2, 24, 10, 12, 128, True, True, False),
+    (1, 64, 8, 64, 64, True, False, False),
+]
+
+
+@pytest.mark.parametrize("case", ENC_CASES)
+def test_encoder_conv_backward(case, hip_device):
+    n, cin, h, w, cout, want_act, want_pool, first = case
+    x = rnd(1, (n, cin, h, w), 1.0, 0.0)
+    wt = torch.from_numpy(synth.conv_weight(2, cout, cin, 3))
+    b = torch.from_numpy(synth.conv_bias(3, cout))
+    gpre = rnd(4, (n, cout, h, w))
+    gact = rnd(5, (n, cout, h, w))
+    gpool = rnd(6, (n, cout, h // 2, w // 2))
+    # CPU autograd reference
+    xr, wr, br = x.clone().requires_grad_(), wt.clone().requires_grad_(), b.clone().requires_grad_()
+    xin = R.normalization(xr) if first else xr
+    pre = F.conv2d(xin, wr, br, padding=1)
+    act = F.relu(pre)
+    loss = (pre * gpre).sum()
+    if want_act:
+        loss = loss + (act * gact).sum()
+    if want_pool:
+        loss = loss + (F.max_pool2d(act, 2, 2) * gpool).sum()
+    loss.backward()
+    # HIP
+    d = hip_device
+    xd = x.to(d).requires_grad_()
+    wd = wt.to(d).requires_grad_()
+    bd = b.to(d).requires_grad_()
+    from arbitrarystyletransfer_amd import ops
+    packed = ops.pack_conv3x3(wd.detach())
+    mean = torch.tensor(R.IMNET_MEAN, device=d) if first else None
+    std = torch.tensor(R.IMNET_STD, device=d) if first else None
+    p, a, q = Fn.EncoderConvFn.apply(xd, wd, bd, packed, want_act, want_pool, mean, std)
+    lg = (p * gpre.to(d)).sum()
+    if want_act:
+        lg = lg + (a * gact.to(d)).sum()
+    if want_pool:
+        lg = lg + (q * gpool.to(d)).sum()
+    lg.backward()
+    assert rel_inf(xd.grad, xr.grad) <= TOL
+    assert rel_inf(wd.grad, wr.grad) <= TOL
+    assert rel_inf(bd.grad, br.grad) <= TOL
+
+
+DEC_CASES = [
+    # n, cin, h_in, w_in, cout, up, relu
+    (2, 16, 8, 12, 64, 1, True),
+    (1, 32, 6, 8, 64, 2, True),
+    (2, 8, 5, 7, 128, 2, False),
+    (1, 64, 16, 32, 3, 1, False),   # final decoder conv
+    (1, 4, 2, 2, 64, 1, True),      # smallest reflect-padded map
+    (1, 12, 1, 3, 64, 2, True),     # upsampled 1-row map
+]
+
+
+@pytest.mark.parametrize("case", DEC_CASES)
+def test_decoder_conv_backward(case, hip_device):
+    n, cin, h, w, cout, up, relu = case
+    x = rnd(11, (n, cin, h, w), 1.0, 0.2)
+    wt = torch.from_numpy(synth.conv_weight(12, cout, cin, 3))
+    b = torch.from_numpy(synth.conv_bias(13, cout))
+    g = rnd(14, (n, cout, h * up, w * up))
+    xr, wr, br = x.clone().requires_grad_(), wt.clone().requires_grad_(), b.clone().requires_grad_()
+    y = xr
+    if up == 2:
+        y = F.interpolate(y, scale_factor=2, mode="nearest")
+    y = F.conv2d(F.pad(y, (1, 1, 1, 1), mode="reflect"), wr, br)
+    if relu:
+        y = F.relu(y)
+    (y * g).sum().backward()
+    d = hip_device
+    xd, wd, bd = x.to(d).requires_grad_(), wt.to(d).requires_grad_(), b.to(d).requires_grad_()
+    from arbitrarystyletransfer_amd import ops
+    yd = Fn.DecoderConvFn.apply(xd, wd, bd, ops.pack_conv3x3(wd.detach()), up, relu)
+    assert rel_inf(yd, y) <= 2e-5
+    (yd * g.to(d)).sum().backward()
+    assert rel_inf(xd.grad, xr.grad) <= TOL
+    assert rel_inf(wd.grad, wr.grad) <= TOL
+    assert rel_inf(bd.grad, br.grad) <= TOL
+
+
+def test_loss_functions_golden(golden, hip_device):
+    g = golden("losses")
+    d = hip_device
+    a = torch.from_numpy(g["a"]).to(d).requires_grad_()
+    b = torch.from_numpy(g["b"]).to(d)
+    gm = L.gram_matrix(a)
+    assert rel_inf(gm, g["gram"]) <= TOL
+    (gm * torch.arange(gm.numel(), dtype=torch.float32, device=d).view_as(gm)).sum().backward()
+    assert rel_inf(a.grad, g["gram_grad"]) <= TOL
+    a.grad = None
+    sl = L.compute_style_loss(a, b)
+    sl.backward()
+    np.testing.assert_allclose(sl.item(), float(g["style_loss"]), rtol=1e-5)
+    assert rel_inf(a.grad, g["style_grad"]) <= TOL
+    a.grad = None
+    cl = L.compute_content_loss(models.mean_variance_norm(a), models.mean_variance_norm(b))
+    cl.backward()
+    np.testing.assert_allclose(cl.item(), float(g["content_loss"]), rtol=1e-5)
+    assert rel_inf(a.grad, g["content_grad"]) <= TOL
+    a.grad = None
+    cf = L.content_mvn_loss(a, b)   # fused form of the same term
+    cf.backward()
+    np.testing.assert_allclose(cf.item(), float(g["content_loss"]), rtol=1e-5)
+    assert rel_inf(a.grad, g["content_grad"]) <= TOL
+    img = torch.from_numpy(g["img"]).to(d).requires_grad_()
+    tv = L.tv_loss(img)
+    tv.backward()
+    np.testing.assert_allclose(tv.item(), float(g["tv"]), rtol=1e-5)
+    assert rel_inf(img.grad, g["tv_grad"]) <= TOL
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 32, 32), (1, 512, 8, 8), (3, 3, 20, 28)])
+def test_style_loss_vs_oracle(shape, hip_device):
+    x = rnd(21, shape, 1.0, 0.5)
+    y = rnd(22, shape, 1.2, 0.4)
+    xr = x.clone().requires_grad_()
+    ref = R.compute_style_loss(xr, y) * 0.75
+    ref.backward()
+    xd = x.to(hip_device).requires_grad_()
+    got = L.style_loss_weighted(xd, y.to(hip_device), 0.75)
+    got.backward()
+    np.testing.assert_allclose(got.item(), ref.item(), rtol=2e-5)
+    assert rel_inf(xd.grad, xr.grad) <= TOL
+
+
+def test_channel_stats_backward(hip_device):
+    x = rnd(31, (2, 5, 7, 9), 2.0, 1.0)
+    gm, gs = rnd(32, (2, 5, 1, 1)), rnd(33, (2, 5, 1, 1))
+    xr = x.clone().requires_grad_()
+    m, s = R.calc_mean_std(xr)
+    ((m * gm).sum() + (s * gs).sum()).backward()
+    xd = x.to(hip_device).requires_grad_()
+    md, sd = models.calc_mean_std(xd)
+    ((md * gm.to(hip_device)).sum() + (sd * gs.to(hip_device)).sum()).backward()
+    assert rel_inf(xd.grad, xr.grad) <= TOL
+
+
+def test_fused_adam_matches_torch(hip_device):
+    shapes = [(64, 3, 3, 3), (64,), (300001,), (7, 5)]
+    ps = [rnd(40 + i, s, 0.1) for i, s in enumerate(shapes)]
+    ref = [p.clone().requires_grad_() for p in ps]
+    got = [torch.nn.Parameter(p.to(hip_device)) for p in ps]
+    opt_r = torch.optim.Adam(ref, lr=2e-4, betas=[0.9, 0.999], eps=1e-5)
+    opt_g = optim.FusedAdam(got, lr=2e-4, betas=(0.9, 0.999), eps=1e-5, max_grad_norm=2.0,
+                            error_if_nonfinite=True)
+    for step in range(3):
+        grads = [rnd(100 + 10 * step + i, s, 3.0) for i, s in enumerate(shapes)]
+        for p, g in zip(ref, grads):
+            p.grad = g.clone()
+        for p, g in zip(got, grads):
+            p.grad = g.to(hip_device)
+        norm_r = torch.nn.utils.clip_grad_norm_(ref, 2.0, error_if_nonfinite=True)
+        opt_r.step()
+        opt_g.step()
+        np.testing.assert_allclose(opt_g.last_grad_norm.item(), norm_r.item(), rtol=1e-5)
+        for p, q in zip(got, ref):
+            np.testing.assert_allclose(p.detach().cpu().numpy(), q.detach().numpy(), rtol=0, atol=2e-7)
+    with pytest.raises(RuntimeError):
+        got[0].grad = torch.full_like(got[0], float("nan"))
+        for p in got[1:]:
+            p.grad = torch.zeros_like(p)
+        opt_g.step()
+
+
+def test_train_step_golden(golden, hip_device):
+    from arbitrarystyletransfer_amd.train import AdaINTrainer, default_args
+    g = golden("train_step_64")
+    d = hip_device
+    snap = {}
+
+    def hook(params):
+        snap["grads"] = [p.grad.detach().clone() for p in params]
+
+    tr = AdaINTrainer(default_args(batch_size=2), device=d, grad_hook=hook)
+    out = tr.train_step(torch.from_numpy(g["content"]).to(d), torch.from_numpy(g["style"]).to(d))
+    for k in ("content_loss", "style_loss", "lf_loss", "tv_loss", "loss"):
+        np.testing.assert_allclose(out[k].item(), float(g[k]), rtol=1e-4, err_msg=k)
+    np.testing.assert_allclose(out["grad_norm"].item(), float(g["grad_norm"]), rtol=1e-4)
+    assert rel_inf(out["stylized"], g["stylized"]) <= 1e-4
+    for i, (gr, p) in enumerate(zip(snap["grads"], tr.params)):
+        gs = gr.double()
+        ref = g[f"grad{i}_sum"]
+        np.testing.assert_allclose(gs.abs().sum().item(), ref[1], rtol=2e-3, err_msg=f"grad{i}")
+        np.testing.assert_allclose(gs.sum().item(), ref[0], rtol=2e-3, atol=2e-3 * ref[1], err_msg=f"grad{i}")
+        got_p = p.detach().cpu()
+        got_p = got_p.numpy() if got_p.numel() <= 4096 else got_p.reshape(-1)[::97].numpy()
+        np.testing.assert_allclose(got_p, g[f"param{i}"], rtol=0, atol=2e-6, err_msg=f"param{i}")
+    # a second step runs on the updated (re-packed) weights
+    out2 = tr.train_step(torch.from_numpy(g["content"]).to(d), torch.from_numpy(g["style"]).to(d))
+    assert torch.isfinite(out2["loss"]) and out2["loss"].item() != out["loss"].item()
+
+
+def test_dp_arena_adopts_kernel_gradients(hip_device):
+    """With a gradient arena registered, the decoder's weight gradients are views of one flat
+    buffer (no copy), ready for a single all-reduce."""
+    from arbitrarystyletransfer_amd.dp import FlatGradArena
+    dec = models.VGGDecoder().to(hip_device)
+    arena = FlatGradArena(list(dec.parameters()))
+    try:
+        t = rnd(50, (1, 512, 4, 4), 0.5, 0.5).to(hip_device)
+        dec(t).sum().backward()
+        for p in dec.parameters():
+            assert p.grad is not None and p.grad.data_ptr() == arena.view_for(p).data_ptr()
+        arena.all_reduce()  # world size 1: no-op
+        assert torch.isfinite(arena.flat).all()
+    finally:
+        arena.unregister()

@@ -125,3 +125,19 @@ def test_losses(golden):
     tv.backward()
     np.testing.assert_allclose(tv.item(), float(g["tv"]), rtol=1e-5)
     np.testing.assert_allclose(img.grad.numpy(), g["tv_grad"], rtol=1e-5, atol=1e-6)
+
+
+def test_train_step_64(golden):
+    g = golden("train_step_64")
+    dec = [(T(w).clone(), T(b).clone()) for w, b in _dec()]
+    out = R.train_step(T(g["content"]), T(g["style"]), _enc(), dec)
+    for k in ("content_loss", "style_loss", "lf_loss", "tv_loss", "loss", "grad_norm"):
+        np.testing.assert_allclose(float(out[k]), float(g[k]), rtol=1e-5, err_msg=k)
+    assert rel_inf(out["stylized"].detach(), g["stylized"]) < 1e-5
+    for i, (gr, p) in enumerate(zip(out["grads"], out["params"])):
+        gs = gr.double()
+        np.testing.assert_allclose([gs.sum().item(), gs.abs().sum().item()], g[f"grad{i}_sum"], rtol=1e-4,
+                                   atol=1e-6 * float(g[f"grad{i}_sum"][1]))
+        ref_p = g[f"param{i}"]
+        got_p = p.numpy() if p.numel() <= 4096 else p.reshape(-1)[::97].numpy()
+        np.testing.assert_allclose(got_p, ref_p, rtol=0, atol=1e-6)
