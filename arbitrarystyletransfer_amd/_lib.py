@@ -34,12 +34,14 @@ SIGNATURES = {
     "ast_conv3x3_pack_weights_ex_f32": (_i, [_p, _p, _i, _i, _i, _p, _p]),
     "ast_conv_act_backward_f32": (_i, [_p, _p, _p, _p, _p, _ll, _i, _i, _p]),
     "ast_relu_mask_f32": (_i, [_p, _p, _p, _ll, _p]),
-    "ast_conv3x3_dgrad_border_f32": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _p]),
-    "ast_pad_up_adjoint_f32": (_i, [_p, _p, _p, _p, _ll, _i, _i, _i, _p]),
+    "ast_grad_pad_f32": (_i, [_p, _p, _p, _ll, _i, _i, _i, _p]),
+    "ast_pad_up_adjoint_f32": (_i, [_p, _p, _ll, _i, _i, _i, _i, _p]),
     "ast_conv3x3_wgrad_f32": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "ast_conv3x3_wgrad_ex_f32": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _ll, _ll, _p]),
     "ast_gram_f32": (_i, [_p, _p, _i, _i, _ll, _f, _p]),
     "ast_gram_backward_f32": (_i, [_p, _p, _p, _p, _p, _i, _i, _ll, _f, _p, _i, _p]),
-    "ast_mvn_huber_f32": (_i, [_p, _p, _ll, _ll, _f, _p, _p, _p, _i, _p]),
+    "ast_mvn_huber_f32": (_i, [_p, _p, _ll, _ll, _f, _p, _p, _p]),
+    "ast_mvn_huber_backward_f32": (_i, [_p, _p, _p, _ll, _ll, _f, _p, _p, _i, _p]),
     "ast_huber_f32": (_i, [_p, _p, _ll, _f, _p, _p, _p, _i, _p]),
     "ast_style_moments_f32": (_i, [_p, _p, _ll, _ll, _f, _p, _p, _p, _p, _p, _p]),
     "ast_gram_huber_f32": (_i, [_p, _p, _ll, _f, _p, _p, _p, _p]),

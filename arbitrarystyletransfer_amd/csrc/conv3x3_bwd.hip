@@ -1,16 +1,20 @@
 // Backward of the 3x3 conv blocks for gfx950 (training step).
 //
-// Input gradient ("dgrad"): dX = conv3x3_same(dY, W^T flipped) with zero padding — the forward
-// MFMA kernel run on a transposed+flipped weight pack (ast_conv3x3_pack_weights_ex_f32). For the
-// decoder's [Upsample] + ReflectionPad + Conv that gives the gradient of the *padded* input at
-// its interior; the 4 border lines are computed here (dgrad_border_kernel) and the reflect-pad /
-// nearest-upsample adjoint folds everything back onto the source grid (pad_up_adjoint_kernel).
+// Input gradient ("dgrad"): the forward MFMA kernel run on a transposed+flipped weight pack
+// (ast_conv3x3_pack_weights_ex_f32).
+//  * Zero-padded convs (VGG encoder / loss network): dX = conv3x3_same(dY, W') directly.
+//  * Decoder [Upsample] + ReflectionPad + Conv: the ReLU-masked output gradient is written into a
+//    zero-padded buffer (pad_grad_kernel), so one "same" conv over it yields the FULL gradient of
+//    the reflect-padded input, borders included; the reflect-pad / nearest-upsample adjoint then
+//    folds it onto the source grid (pad_up_adjoint_full_kernel).
 //
 // Weight gradient ("wgrad"): dW[co][ci][tap] = sum_pix dY[co][pix] * P[ci][pix+tap] as an MFMA
-// fp32 GEMM with K = pixels: per workgroup 64 output x 32 input channels x 9 taps, looping over a
-// range of 4x32-pixel tiles, fp32 atomics into dW at the end (the pixel range is split across
-// workgroups). P is staged exactly like the forward kernel's source tile (zero/reflect pad and
-// upsample resolved by the LDS read address).
+// fp32 GEMM with K = pixels. A workgroup (4 waves) owns 64 output x 64 input channels x 9 taps;
+// each wave 32 x 32 x 9 taps in 9 accumulators. Per 2x32-pixel tile it stages the input halo tile
+// (same source-tile staging as the forward kernel: zero/reflect pad and upsample resolved by the
+// LDS read address, so the 9 taps are constant offsets) and the dY tile; a workgroup sweeps a
+// range of tiles and adds its partial dW with fp32 atomics (the pixel range is split across
+// workgroups). dY may be read from the padded gradient buffer (pitch/plane/offset).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/ast_hip.h"
@@ -31,10 +35,9 @@ __device__ __forceinline__ int src_index(int g, int n, int reflect) {
 }
 
 // wp[ci_pad][9][co_pad] layout of the forward pack, but for the transposed+flipped filter:
-// W'[o=ci][i=co][ky][kx] = W[co][ci][2-ky][2-kx] * (row_scale ? row_scale[ci] : 1)
+// W'[o=ci][i=co][ky][kx] = W[co][ci][2-ky][2-kx] / (scale ? scale[ci] : 1)
 __global__ void pack_tf_kernel(const float* __restrict__ w, float* __restrict__ wp, int cout, int cin, int pad_out,
                                int pad_in, const float* __restrict__ scale) {
-  // forward-pack view of W': "cout" = cin, "cin" = cout
   const int64_t total = (int64_t)pad_in * 9 * pad_out;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
@@ -86,63 +89,43 @@ __global__ void act_backward_kernel(const float* __restrict__ pre, const float* 
   }
 }
 
-// Border lines of dP = full correlation of dY (N, Cout, H, W) with W (the gradient of the
-// reflect-padded input at padded rows 0 and H+1 and padded columns 0 and W+1).
-// border layout per (n, ci): [top (W+2)][bottom (W+2)][left (H)][right (H)].
-__global__ void dgrad_border_kernel(const float* __restrict__ dy, const float* __restrict__ w,
-                                    float* __restrict__ border, int N, int Cout, int Cin, int H, int W) {
-  const int L = 2 * (W + 2) + 2 * H;
-  const int64_t total = (int64_t)N * Cin * L;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int e = (int)(idx % L);
-    const int64_t nc = idx / L;
-    const int ci = (int)(nc % Cin);
-    const int n = (int)(nc / Cin);
-    int py, px;
-    if (e < W + 2) { py = 0; px = e; }
-    else if (e < 2 * (W + 2)) { py = H + 1; px = e - (W + 2); }
-    else if (e < 2 * (W + 2) + H) { py = 1 + e - 2 * (W + 2); px = 0; }
-    else { py = 1 + e - 2 * (W + 2) - H; px = W + 1; }
-    // dP[py][px] = sum_{co,ky,kx} dY[co][py-ky][px-kx] * W[co][ci][ky][kx]
-    float s = 0.f;
-    for (int co = 0; co < Cout; ++co) {
-      const float* d = dy + ((int64_t)n * Cout + co) * H * W;
-      const float* wk = w + ((int64_t)co * Cin + ci) * 9;
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        const int oy = py - ky;
-        if (oy < 0 || oy >= H) continue;
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int ox = px - kx;
-          if (ox < 0 || ox >= W) continue;
-          s = fmaf(d[(int64_t)oy * W + ox], wk[ky * 3 + kx], s);
-        }
-      }
+// out_pad [planes, H+2, Wp] = zero-padded (mask > 0 ? g : 0) (mask optional): the output gradient
+// laid out so that a zero-padded "same" conv with the transposed+flipped filter produces the
+// FULL gradient of the reflect-padded input, borders included.
+__global__ void pad_grad_kernel(const float* __restrict__ g, const float* __restrict__ mask, float* __restrict__ out,
+                                int64_t planes, int H, int W, int Wp) {
+  const int64_t n = planes * (H + 2) * Wp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Wp);
+    const int r = (int)((i / Wp) % (H + 2));
+    const int64_t p = i / ((int64_t)(H + 2) * Wp);
+    float v = 0.f;
+    if (r >= 1 && r <= H && c >= 1 && c <= W) {
+      const int64_t s = (p * H + (r - 1)) * W + (c - 1);
+      v = g[s];
+      if (mask && !(mask[s] > 0.f)) v = 0.f;
     }
-    border[idx] = s;
+    out[i] = v;
   }
 }
 
-// dx[v] (source grid, h_in x w_in) = sum over padded positions p mapping onto v of dP[p]:
-//   interior dP[p] = dpin[p-1] (p in [1, H]); border dP from dgrad_border_kernel.
-//   up == 1: p -> u = refl(p-1) = v;   up == 2: p -> u = refl(p-1) -> v = u >> 1.
-// mask (optional, same shape as dx): dx = mask > 0 ? dx : 0 (ReLU of the layer that made x).
-__global__ void pad_up_adjoint_kernel(const float* __restrict__ dpin, const float* __restrict__ border,
-                                      const float* __restrict__ mask, float* __restrict__ dx, int64_t planes,
-                                      int h_in, int w_in, int up) {
+// dx[v] = sum of the full padded-input gradient dP [planes, H+2, Wp] over the padded positions
+// that the reflect pad (and nearest upsample) map onto source pixel v:
+//   up == 1: p -> refl(p-1) = v;   up == 2: p -> refl(p-1) -> v = u >> 1 (refl on the 2x grid).
+__global__ void pad_up_adjoint_full_kernel(const float* __restrict__ dp, float* __restrict__ dx, int64_t planes,
+                                           int h_in, int w_in, int up, int Wp) {
   const int H = h_in * up, W = w_in * up;
-  const int L = 2 * (W + 2) + 2 * H;
   const int64_t total = planes * h_in * w_in;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int vx = (int)(idx % w_in);
     const int vy = (int)((idx / w_in) % h_in);
     const int64_t p = idx / ((int64_t)h_in * w_in);
-    // padded rows/cols (as dP indices) that land on vy / vx
     int rows[4], nr = 0, cols[4], nc = 0;
-    for (int k = 0; k < up; ++k) { rows[nr++] = up * vy + k + 1; cols[nc++] = up * vx + k + 1; }
+    for (int k = 0; k < up; ++k) {
+      rows[nr++] = up * vy + k + 1;
+      cols[nc++] = up * vx + k + 1;
+    }
     if (up == 1) {
       if (vy == 1) rows[nr++] = 0;
       if (vy == H - 2) rows[nr++] = H + 1;
@@ -154,28 +137,15 @@ __global__ void pad_up_adjoint_kernel(const float* __restrict__ dpin, const floa
       if (vx == 0) cols[nc++] = 0;
       if (vx == w_in - 1) cols[nc++] = W + 1;
     }
-    const float* dp = dpin + p * H * W;
-    const float* bd = border + p * L;
+    const float* d = dp + p * (int64_t)(H + 2) * Wp;
     float s = 0.f;
-    for (int a = 0; a < nr; ++a) {
-      const int r = rows[a];
-      for (int b = 0; b < nc; ++b) {
-        const int c = cols[b];
-        float v;
-        if (r == 0) v = bd[c];
-        else if (r == H + 1) v = bd[(W + 2) + c];
-        else if (c == 0) v = bd[2 * (W + 2) + (r - 1)];
-        else if (c == W + 1) v = bd[2 * (W + 2) + H + (r - 1)];
-        else v = dp[(int64_t)(r - 1) * W + (c - 1)];
-        s += v;
-      }
-    }
-    if (mask && !(mask[idx] > 0.f)) s = 0.f;
+    for (int a = 0; a < nr; ++a)
+      for (int b = 0; b < nc; ++b) s += d[(int64_t)rows[a] * Wp + cols[b]];
     dx[idx] = s;
   }
 }
 
-// dx = g * (mask > 0) (ReLU backward for an input gradient with no pad/upsample adjoint).
+// dx = g * (mask > 0) (ReLU backward given the ReLU output).
 __global__ void relu_mask_kernel(const float* __restrict__ g, const float* __restrict__ mask, float* __restrict__ out,
                                  int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -185,33 +155,46 @@ __global__ void relu_mask_kernel(const float* __restrict__ g, const float* __res
 // ------------------------------------------------------------------------------------------
 // Weight gradient.
 // ------------------------------------------------------------------------------------------
-constexpr int WG_CO = 64, WG_CI = 32, WG_TH = 4, WG_TW = 32, WG_PIX = WG_TH * WG_TW;
+constexpr int WG_CO = 64, WG_CI = 64, WG_TH = 2, WG_TW = 32, WG_PIX = WG_TH * WG_TW;
+constexpr int WG_DS = WG_CO + 1;  // dY tile [pix][co] row stride (odd: transposed stores conflict-free)
 
 template <int UP>
 struct WgCfg {
   static constexpr int SW = WG_TW / UP;
   static constexpr int SR = WG_TH / UP + 2;
   static constexpr int RS = SW + 8;
-  static constexpr int PS = SR * RS + 1;     // per-channel plane stride (odd: ci on lanes is conflict-free)
-  static constexpr int DS = WG_PIX + 1;      // per-co stride of the dY tile
-  static constexpr int LDS = (WG_CI * PS + WG_CO * DS) * 4;
+  static constexpr int C0 = 4;
+  static constexpr int PS = SR * RS + 1;  // per-channel plane stride (odd: ci on lanes is conflict-free)
+  static constexpr int QV = SW / 4;
+  static constexpr int LDS = (WG_CI * PS + WG_PIX * WG_DS) * 4;
+};
+
+struct WgArgs {
+  const float* x;
+  const float* dy;
+  float* dw;
+  float* db;
+  int N, Cin, Hin, Win, Cout, reflect;
+  int dy_pitch;        // row stride of dy
+  int64_t dy_plane;    // plane stride of dy
+  int64_t dy_off;      // offset of element (0, 0) inside a plane
+  int tiles_x, tiles_y;
+  int64_t tiles_per_block, ntiles;
 };
 
 template <int UP>
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                                       float* __restrict__ dw, float* __restrict__ db, int N, int Cin,
-                                                       int Hin, int Win, int Cout, int reflect, int tiles_x,
-                                                       int tiles_y, int64_t tiles_per_block, int64_t ntiles) {
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(WgArgs a) {
   using C = WgCfg<UP>;
-  constexpr int SW = C::SW, SR = C::SR, RS = C::RS, PS = C::PS, DS = C::DS;
+  constexpr int SW = C::SW, SR = C::SR, RS = C::RS, PS = C::PS, QV = C::QV, C0 = C::C0;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Ps = smem;                  // [WG_CI][PS]
-  float* Ds = smem + WG_CI * PS;     // [WG_CO][DS]
+  float* Ps = smem;                   // [WG_CI][PS]
+  float* Ds = smem + WG_CI * PS;      // [WG_PIX][WG_DS]
+  const int Hin = a.Hin, Win = a.Win;
   const int H = Hin * UP, W = Win * UP;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-  const int wco = wave & 1, wtap = wave >> 1;      // co half, tap group {0..4} / {5..8}
-  const int co_groups = (Cout + WG_CO - 1) / WG_CO;
-  const int ci_groups = (Cin + WG_CI - 1) / WG_CI;
+  const int wco = wave & 1, wci = wave >> 1;
+  const int co_groups = (a.Cout + WG_CO - 1) / WG_CO;
+  const int ci_groups = (a.Cin + WG_CI - 1) / WG_CI;
   int b = blockIdx.x;
   const int cog = b % co_groups;
   b /= co_groups;
@@ -219,86 +202,109 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const float* __restrict__
   const int64_t split = b / ci_groups;
   const int co0 = cog * WG_CO, ci0 = cig * WG_CI;
 
-  f32x16 acc[5];
+  f32x16 acc[9];
 #pragma unroll
-  for (int t = 0; t < 5; ++t)
+  for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  float bacc = 0.f;  // bias gradient partial (tid < 64 -> co0 + tid), only for cig == 0
+  float bacc = 0.f;  // bias partial: co = tid & 63, pixels of quarter tid >> 6
 
-  const int64_t t0 = split * tiles_per_block;
-  const int64_t t1 = min(ntiles, t0 + tiles_per_block);
+  // per-lane LDS column offsets of the B operand for kx = 0..2 (pixel column parity = h)
+  int bcol[3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) bcol[kx] = (UP == 1) ? (C0 - 1 + h + kx) : (C0 + ((h + kx - 1) >> 1));
+  const float* prow_base = Ps + (wci * 32 + l32) * PS;
+  const int arow = wco * 32 + l32;
+
+  const int64_t t0 = a.tiles_per_block * split;
+  const int64_t t1 = min(a.ntiles, t0 + a.tiles_per_block);
   for (int64_t tile = t0; tile < t1; ++tile) {
     int64_t tt = tile;
-    const int tx = (int)(tt % tiles_x);
-    tt /= tiles_x;
-    const int ty = (int)(tt % tiles_y);
-    const int n = (int)(tt / tiles_y);
+    const int tx = (int)(tt % a.tiles_x);
+    tt /= a.tiles_x;
+    const int ty = (int)(tt % a.tiles_y);
+    const int n = (int)(tt / a.tiles_y);
     const int x0 = tx * WG_TW, y0 = ty * WG_TH;
     const int sx0 = x0 / UP, sy0 = y0 / UP - 1;
+    const float* xin = a.x + (int64_t)n * a.Cin * Hin * Win;
+    const int plane_in = Hin * Win;
     __syncthreads();
-    // stage P (source tile with halo, scalar gather: simple and general)
-    const float* xin = x + (int64_t)n * Cin * Hin * Win;
-    for (int e = tid; e < WG_CI * SR * (SW + 2); e += 256) {
-      const int col = e % (SW + 2);
-      const int cr = e / (SW + 2);
-      const int r = cr % SR, c = cr / SR;
-      const int ci = ci0 + c;
-      const int sy = src_index<UP>(sy0 + r, Hin, reflect);
-      const int sx = src_index<UP>(sx0 - 1 + col, Win, reflect);
-      float v = 0.f;
-      if (ci < Cin && sy >= 0 && sx >= 0) v = xin[(int64_t)ci * Hin * Win + (int64_t)sy * Win + sx];
-      Ps[c * PS + r * RS + 3 + col] = v;
+    // ---- input halo tile [ci][SR][RS] ----
+    if ((sx0 + SW <= Win) && ((Win & 3) == 0)) {
+      for (int e = tid; e < WG_CI * SR * (QV + 2); e += 256) {
+        const int q = e % (QV + 2);
+        const int cr = e / (QV + 2);
+        const int r = cr % SR, c = cr / SR;
+        const int ci = ci0 + c;
+        const int sy = src_index<UP>(sy0 + r, Hin, a.reflect);
+        float* row = Ps + c * PS + r * RS;
+        if (q < QV) {
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ci < a.Cin && sy >= 0) v = *reinterpret_cast<const float4*>(xin + (int64_t)ci * plane_in + sy * Win + sx0 + 4 * q);
+          row[C0 + 4 * q] = v.x; row[C0 + 4 * q + 1] = v.y; row[C0 + 4 * q + 2] = v.z; row[C0 + 4 * q + 3] = v.w;
+        } else {
+          const int sx = src_index<UP>(q == QV ? sx0 - 1 : sx0 + SW, Win, a.reflect);
+          row[q == QV ? C0 - 1 : C0 + SW] =
+              (ci < a.Cin && sy >= 0 && sx >= 0) ? xin[(int64_t)ci * plane_in + sy * Win + sx] : 0.f;
+        }
+      }
+    } else {
+      for (int e = tid; e < WG_CI * SR * (SW + 2); e += 256) {
+        const int col = e % (SW + 2);
+        const int cr = e / (SW + 2);
+        const int r = cr % SR, c = cr / SR;
+        const int ci = ci0 + c;
+        const int sy = src_index<UP>(sy0 + r, Hin, a.reflect);
+        const int sx = src_index<UP>(sx0 - 1 + col, Win, a.reflect);
+        Ps[c * PS + r * RS + C0 - 1 + col] =
+            (ci < a.Cin && sy >= 0 && sx >= 0) ? xin[(int64_t)ci * plane_in + sy * Win + sx] : 0.f;
+      }
     }
-    // stage dY tile [co][pix] (pix = row*32 + col), zero outside
-    const float* dyn = dy + (int64_t)n * Cout * H * W;
+    // ---- dY tile [pix][co] (pix = row*32 + col), zero outside ----
+    const float* dyn = a.dy + (int64_t)n * a.Cout * a.dy_plane + a.dy_off;
     for (int e = tid; e < WG_CO * WG_PIX; e += 256) {
       const int pix = e % WG_PIX, c = e / WG_PIX;
       const int co = co0 + c, yy = y0 + pix / WG_TW, xx = x0 + pix % WG_TW;
       float v = 0.f;
-      if (co < Cout && yy < H && xx < W) v = dyn[(int64_t)co * H * W + (int64_t)yy * W + xx];
-      Ds[c * DS + pix] = v;
+      if (co < a.Cout && yy < H && xx < W) v = dyn[(int64_t)co * a.dy_plane + (int64_t)yy * a.dy_pitch + xx];
+      Ds[pix * WG_DS + c] = v;
     }
     __syncthreads();
-    if (cig == 0 && tid < WG_CO) {
-      float s = 0.f;
-      for (int pix = 0; pix < WG_PIX; ++pix) s += Ds[tid * DS + pix];
-      bacc += s;
+    if (a.db && cig == 0) {
+      const int c = tid & 63, q = tid >> 6;
+#pragma unroll
+      for (int k = 0; k < WG_PIX / 4; ++k) bacc += Ds[(q * (WG_PIX / 4) + k) * WG_DS + c];
     }
-    // K loop over pixel pairs
 #pragma unroll 2
     for (int kp = 0; kp < WG_PIX / 2; ++kp) {
-      const int pix = 2 * kp + h;
-      const int prow = pix / WG_TW, pcol = pix % WG_TW;
-      const float a = Ds[(wco * 32 + l32) * DS + pix];
+      const int prow = (2 * kp) / WG_TW;   // wave-uniform
+      const int pc0 = (2 * kp) % WG_TW;    // even; the lane's pixel column is pc0 + h
+      const float av = Ds[(2 * kp + h) * WG_DS + arow];
 #pragma unroll
-      for (int t = 0; t < 5; ++t) {
-        const int tap = wtap * 5 + t;
-        if (tap < 9) {
-          const int ky = tap / 3, kx = tap % 3;
-          const int orow = prow + ky - 1;
-          const int srow = (UP == 1) ? orow + 1 : (orow >> 1) + 1;
-          const int scol = 3 + (((x0 + pcol + kx - 1) >> (UP - 1)) - sx0 + 1);
-          const float bv = Ps[l32 * PS + srow * RS + scol];
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc[t], 0, 0, 0);
+      for (int ky = 0; ky < 3; ++ky) {
+        const int srow = (UP == 1) ? prow + ky : ((prow + ky - 1) >> 1) + 1;
+        const float* rp = prow_base + srow * RS + ((UP == 1) ? pc0 : (pc0 >> 1));
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const float bv = rp[bcol[kx]];
+          acc[ky * 3 + kx] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[ky * 3 + kx], 0, 0, 0);
         }
       }
     }
   }
   // C[i = co][j = ci]: col j = l32, rows i = (r&3)+8(r>>2)+4h
+  const int ci = ci0 + wci * 32 + l32;
+  if (ci < a.Cin) {
 #pragma unroll
-  for (int t = 0; t < 5; ++t) {
-    const int tap = wtap * 5 + t;
-    if (tap >= 9) continue;
-    const int ci = ci0 + l32;
-    if (ci >= Cin) continue;
+    for (int t = 0; t < 9; ++t) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (co < Cout) atomicAdd(dw + ((int64_t)co * Cin + ci) * 9 + tap, acc[t][r]);
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (co < a.Cout) atomicAdd(a.dw + ((int64_t)co * a.Cin + ci) * 9 + t, acc[t][r]);
+      }
     }
   }
-  if (db && cig == 0 && tid < WG_CO && co0 + tid < Cout) atomicAdd(db + co0 + tid, bacc);
+  if (a.db && cig == 0 && co0 + (tid & 63) < a.Cout) atomicAdd(a.db + co0 + (tid & 63), bacc);
 }
 
 int grid1(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
@@ -340,35 +346,41 @@ int ast_relu_mask_f32(const float* g, const float* mask, float* out, long long n
   return (int)hipGetLastError();
 }
 
-int ast_conv3x3_dgrad_border_f32(const float* dy, const float* w, float* border, int n, int cout, int cin, int h,
-                                 int w_, void* stream) {
-  if (!dy || !w || !border) return AST_E_NULLPTR;
-  if (n <= 0 || cout <= 0 || cin <= 0 || h <= 0 || w_ <= 0) return AST_E_SHAPE;
-  const int64_t total = (int64_t)n * cin * (2 * (w_ + 2) + 2 * h);
-  hipLaunchKernelGGL(dgrad_border_kernel, dim3(grid1(total)), dim3(256), 0, (hipStream_t)stream, dy, w, border, n,
-                     cout, cin, h, w_);
+int ast_grad_pad_f32(const float* g, const float* mask, float* out_pad, long long planes, int h, int w, int pitch,
+                     void* stream) {
+  if (!g || !out_pad) return AST_E_NULLPTR;
+  if (planes <= 0 || h <= 0 || w <= 0 || pitch < w + 2) return AST_E_SHAPE;
+  hipLaunchKernelGGL(pad_grad_kernel, dim3(grid1(planes * (h + 2) * pitch)), dim3(256), 0, (hipStream_t)stream, g,
+                     mask, out_pad, (int64_t)planes, h, w, pitch);
   return (int)hipGetLastError();
 }
 
-int ast_pad_up_adjoint_f32(const float* dp_interior, const float* border, const float* mask, float* dx,
-                           long long planes, int h_in, int w_in, int upsample, void* stream) {
-  if (!dp_interior || !border || !dx) return AST_E_NULLPTR;
+int ast_pad_up_adjoint_f32(const float* dp_full, float* dx, long long planes, int h_in, int w_in, int upsample,
+                           int pitch, void* stream) {
+  if (!dp_full || !dx) return AST_E_NULLPTR;
   if (planes <= 0 || h_in <= 0 || w_in <= 0) return AST_E_SHAPE;
   if (upsample != 1 && upsample != 2) return AST_E_UNSUPPORTED;
-  if (h_in * upsample < 2 || w_in * upsample < 2) return AST_E_SHAPE;
-  hipLaunchKernelGGL(pad_up_adjoint_kernel, dim3(grid1(planes * h_in * w_in)), dim3(256), 0, (hipStream_t)stream,
-                     dp_interior, border, mask, dx, (int64_t)planes, h_in, w_in, upsample);
+  if (h_in * upsample < 2 || w_in * upsample < 2 || pitch < w_in * upsample + 2) return AST_E_SHAPE;
+  hipLaunchKernelGGL(pad_up_adjoint_full_kernel, dim3(grid1(planes * h_in * w_in)), dim3(256), 0, (hipStream_t)stream,
+                     dp_full, dx, (int64_t)planes, h_in, w_in, upsample, pitch);
   return (int)hipGetLastError();
 }
 
-int ast_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, float* db, int n, int cin, int h_in, int w_in,
-                          int cout, int upsample, int pad_mode, void* stream) {
+int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* db, int n, int cin, int h_in,
+                             int w_in, int cout, int upsample, int pad_mode, int dy_pitch, long long dy_plane,
+                             long long dy_offset, void* stream) {
   if (!x || !dy || !dw) return AST_E_NULLPTR;
   if (n <= 0 || cin <= 0 || h_in <= 0 || w_in <= 0 || cout <= 0) return AST_E_SHAPE;
   if (upsample != 1 && upsample != 2) return AST_E_UNSUPPORTED;
   if (pad_mode != 0 && pad_mode != 1) return AST_E_UNSUPPORTED;
   const int H = h_in * upsample, W = w_in * upsample;
   if (pad_mode == 1 && (H < 2 || W < 2)) return AST_E_SHAPE;
+  if (dy_pitch == 0) {
+    dy_pitch = W;
+    dy_plane = (long long)H * W;
+    dy_offset = 0;
+  }
+  if (dy_pitch < W || dy_plane < (long long)H * dy_pitch || dy_offset < 0) return AST_E_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * (size_t)cout * cin * 9, s);
   if (e != hipSuccess) return (int)e;
@@ -376,23 +388,30 @@ int ast_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, float* db,
     e = hipMemsetAsync(db, 0, sizeof(float) * (size_t)cout, s);
     if (e != hipSuccess) return (int)e;
   }
-  const int tiles_x = cdiv(W, WG_TW), tiles_y = cdiv(H, WG_TH);
-  const int64_t ntiles = (int64_t)tiles_x * tiles_y * n;
+  WgArgs a{};
+  a.x = x; a.dy = dy; a.dw = dw; a.db = db;
+  a.N = n; a.Cin = cin; a.Hin = h_in; a.Win = w_in; a.Cout = cout; a.reflect = pad_mode;
+  a.dy_pitch = dy_pitch; a.dy_plane = dy_plane; a.dy_off = dy_offset;
+  a.tiles_x = cdiv(W, WG_TW);
+  a.tiles_y = cdiv(H, WG_TH);
+  a.ntiles = (int64_t)a.tiles_x * a.tiles_y * n;
   const int groups = cdiv(cout, WG_CO) * cdiv(cin, WG_CI);
-  // ~2048 workgroups; each sweeps a contiguous range of pixel tiles
-  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(ntiles, (2048 + groups - 1) / groups));
-  const int64_t per = (ntiles + splits - 1) / splits;
-  splits = (ntiles + per - 1) / per;
+  // ~1024 workgroups (4 per CU); each sweeps a contiguous range of pixel tiles
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(a.ntiles, (1024 + groups - 1) / groups));
+  a.tiles_per_block = (a.ntiles + splits - 1) / splits;
+  splits = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
   const int64_t nblk = splits * groups;
   if (nblk >= 0x7fffffff) return AST_E_SHAPE;
-  if (upsample == 2) {
-    hipLaunchKernelGGL(wgrad_kernel<2>, dim3((unsigned)nblk), dim3(256), WgCfg<2>::LDS, s, x, dy, dw, db, n, cin,
-                       h_in, w_in, cout, pad_mode, tiles_x, tiles_y, per, ntiles);
-  } else {
-    hipLaunchKernelGGL(wgrad_kernel<1>, dim3((unsigned)nblk), dim3(256), WgCfg<1>::LDS, s, x, dy, dw, db, n, cin,
-                       h_in, w_in, cout, pad_mode, tiles_x, tiles_y, per, ntiles);
-  }
+  if (upsample == 2)
+    hipLaunchKernelGGL(wgrad_kernel<2>, dim3((unsigned)nblk), dim3(256), WgCfg<2>::LDS, s, a);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<1>, dim3((unsigned)nblk), dim3(256), WgCfg<1>::LDS, s, a);
   return (int)hipGetLastError();
+}
+
+int ast_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, float* db, int n, int cin, int h_in, int w_in,
+                          int cout, int upsample, int pad_mode, void* stream) {
+  return ast_conv3x3_wgrad_ex_f32(x, dy, dw, db, n, cin, h_in, w_in, cout, upsample, pad_mode, 0, 0, 0, stream);
 }
 
 }  // extern "C"

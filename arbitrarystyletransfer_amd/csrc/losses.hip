@@ -54,22 +54,83 @@ __device__ void plane_mean_std(const float* __restrict__ p, int64_t n, float eps
 
 __device__ __forceinline__ float gs(const float* g) { return g ? *g : 1.f; }
 
+// One-pass plane moments: every thread keeps shifted sums around its own first element, the
+// (count, mean, M2) triples are merged with Chan's parallel formula across lanes and waves.
+struct Mom {
+  float n, mean, m2;
+};
+
+__device__ __forceinline__ Mom mom_merge(Mom a, Mom b) {
+  const float n = a.n + b.n;
+  if (b.n == 0.f) return a;
+  if (a.n == 0.f) return b;
+  const float d = b.mean - a.mean, f = b.n / n;
+  return {n, a.mean + d * f, a.m2 + b.m2 + d * d * a.n * f};
+}
+
+__device__ __forceinline__ Mom mom_block(Mom m, float* sh) {  // sh: 12 floats
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Mom t{__shfl_xor(m.n, o, 64), __shfl_xor(m.mean, o, 64), __shfl_xor(m.m2, o, 64)};
+    m = mom_merge(m, t);
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    sh[3 * w] = m.n;
+    sh[3 * w + 1] = m.mean;
+    sh[3 * w + 2] = m.m2;
+  }
+  __syncthreads();
+  Mom r{sh[0], sh[1], sh[2]};
+#pragma unroll
+  for (int w = 1; w < 4; ++w) r = mom_merge(r, Mom{sh[3 * w], sh[3 * w + 1], sh[3 * w + 2]});
+  return r;
+}
+
+// mean and sqrt(M2/(n-1) + eps) of two planes in ONE read of each.
+__device__ void plane_mean_std2(const float* __restrict__ p, const float* __restrict__ q, int64_t n, float eps,
+                                float* sh, float& mp, float& sp, float& mq, float& sq) {
+  float kp = 0.f, kq = 0.f, s1p = 0.f, s2p = 0.f, s1q = 0.f, s2q = 0.f, c = 0.f;
+  const int64_t i0 = threadIdx.x;
+  if (i0 < n) {
+    kp = p[i0];
+    kq = q[i0];
+  }
+  for (int64_t i = i0; i < n; i += kThreads) {
+    const float a = p[i] - kp, b = q[i] - kq;
+    s1p += a;
+    s2p += a * a;
+    s1q += b;
+    s2q += b * b;
+    c += 1.f;
+  }
+  Mom A{c, c > 0.f ? kp + s1p / c : 0.f, c > 0.f ? fmaxf(s2p - s1p * s1p / c, 0.f) : 0.f};
+  Mom B{c, c > 0.f ? kq + s1q / c : 0.f, c > 0.f ? fmaxf(s2q - s1q * s1q / c, 0.f) : 0.f};
+  A = mom_block(A, sh);
+  B = mom_block(B, sh);
+  mp = A.mean;
+  sp = sqrtf(A.m2 / (float)(n - 1) + eps);
+  mq = B.mean;
+  sq = sqrtf(B.m2 / (float)(n - 1) + eps);
+}
+
 // ------------------------------------------------------------------------------------------
 // Content term: w * huber(mvn(x), mvn(y)) (mean over all elements), dx += d/dx.
 // mvn z = (x-mu)/sigma, sigma = sqrt(var_unbiased + 1e-5). With g = dL/dz:
 //   dx = (g - mean(g) - z * sum(g z)/(N-1)) / sigma.
 // ------------------------------------------------------------------------------------------
+// Forward: one read of x and y for both planes' moments, one for the Huber sums. With pstats,
+// also keeps per plane (mu_x, sd_x, mu_y, sd_y, mean(g), sum(g z)/(N-1)) for the backward.
 __global__ __launch_bounds__(kThreads) void mvn_huber_kernel(const float* __restrict__ x, const float* __restrict__ y,
-                                                             int64_t hw, float inv_numel, float w,
-                                                             const float* __restrict__ gscale, float* loss,
-                                                             float* __restrict__ dx, int accumulate) {
-  __shared__ float sh[4];
+                                                             int64_t hw, float inv_numel, float w, float* loss,
+                                                             float* __restrict__ pstats) {
+  __shared__ float sh[12];
   const int64_t p = blockIdx.x;
   const float* xp = x + p * hw;
   const float* yp = y + p * hw;
   float mx, sx, my, sy;
-  plane_mean_std(xp, hw, 1e-5f, sh, mx, sx);
-  plane_mean_std(yp, hw, 1e-5f, sh, my, sy);
+  plane_mean_std2(xp, yp, hw, 1e-5f, sh, mx, sx, my, sy);
   float sh_ = 0.f, sg = 0.f, sgz = 0.f;
   for (int64_t i = threadIdx.x; i < hw; i += kThreads) {
     const float z = (xp[i] - mx) / sx;
@@ -81,17 +142,28 @@ __global__ __launch_bounds__(kThreads) void mvn_huber_kernel(const float* __rest
   }
   const float H = block_sum(sh_, sh);
   if (threadIdx.x == 0 && loss) atomicAdd(loss, w * H * inv_numel);
-  if (!dx) return;
+  if (!pstats) return;
   const float G = block_sum(sg, sh);
   const float GZ = block_sum(sgz, sh);
-  const float c = w * inv_numel * gs(gscale);
-  const float gmean = G / (float)hw, gz = GZ / (float)(hw - 1);
-  float* dp = dx + p * hw;
-  for (int64_t i = threadIdx.x; i < hw; i += kThreads) {
-    const float z = (xp[i] - mx) / sx;
-    const float d = z - (yp[i] - my) / sy;
-    const float v = c * (huber_grad(d) - gmean - z * gz) / sx;
-    dp[i] = accumulate ? dp[i] + v : v;
+  if (threadIdx.x == 0) {
+    float* s = pstats + 6 * p;
+    s[0] = mx; s[1] = sx; s[2] = my; s[3] = sy;
+    s[4] = G / (float)hw;
+    s[5] = GZ / (float)(hw - 1);
+  }
+}
+
+// Backward: dx = c * (huber'(d) - mean(g) - z * sum(g z)/(N-1)) / sd_x, one read of x and y.
+__global__ void mvn_huber_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                     const float* __restrict__ pstats, int64_t hw, int64_t n, float c,
+                                     const float* __restrict__ gscale, float* __restrict__ dx, int accumulate) {
+  const float cc = c * gs(gscale);
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    const float* s = pstats + 6 * (i / hw);
+    const float z = (x[i] - s[0]) / s[1];
+    const float d = z - (y[i] - s[2]) / s[3];
+    const float v = cc * (huber_grad(d) - s[4] - z * s[5]) / s[1];
+    dx[i] = accumulate ? dx[i] + v : v;
   }
 }
 
@@ -156,11 +228,10 @@ __global__ void huber_kernel(const float* __restrict__ x, const float* __restric
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void style_stats_kernel(const float* __restrict__ x, const float* __restrict__ y,
                                                                int64_t hw, float* __restrict__ stats) {
-  __shared__ float sh[4];
+  __shared__ float sh[12];
   const int64_t p = blockIdx.x;
   float mx, sx, my, sy;
-  plane_mean_std(x + p * hw, hw, 0.f, sh, mx, sx);
-  plane_mean_std(y + p * hw, hw, 0.f, sh, my, sy);
+  plane_mean_std2(x + p * hw, y + p * hw, hw, 0.f, sh, mx, sx, my, sy);
   if (threadIdx.x == 0) {
     stats[4 * p + 0] = mx;
     stats[4 * p + 1] = sx;
@@ -425,12 +496,23 @@ int ast_gram_backward_f32(const float* feat, const float* dgram, float* dfeat, c
   return (int)hipGetLastError();
 }
 
-int ast_mvn_huber_f32(const float* x, const float* y, long long planes, long long hw, float weight,
-                      const float* gscale, float* loss, float* dx, int accumulate, void* stream) {
+int ast_mvn_huber_f32(const float* x, const float* y, long long planes, long long hw, float weight, float* loss,
+                      float* pstats, void* stream) {
   if (!x || !y) return AST_E_NULLPTR;
   if (planes <= 0 || hw <= 1 || planes > 0x7fffffffLL) return AST_E_SHAPE;
   hipLaunchKernelGGL(mvn_huber_kernel, dim3((unsigned)planes), dim3(kThreads), 0, (hipStream_t)stream, x, y,
-                     (int64_t)hw, (float)(1.0 / ((double)planes * hw)), weight, gscale, loss, dx, accumulate ? 1 : 0);
+                     (int64_t)hw, (float)(1.0 / ((double)planes * hw)), weight, loss, pstats);
+  return (int)hipGetLastError();
+}
+
+int ast_mvn_huber_backward_f32(const float* x, const float* y, const float* pstats, long long planes, long long hw,
+                               float weight, const float* gscale, float* dx, int accumulate, void* stream) {
+  if (!x || !y || !pstats || !dx) return AST_E_NULLPTR;
+  if (planes <= 0 || hw <= 1) return AST_E_SHAPE;
+  const int64_t n = (int64_t)planes * hw;
+  hipLaunchKernelGGL(mvn_huber_bwd_kernel, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, x, y, pstats,
+                     (int64_t)hw, n, (float)((double)weight / ((double)planes * hw)), gscale, dx,
+                     accumulate ? 1 : 0);
   return (int)hipGetLastError();
 }
 

@@ -68,16 +68,21 @@ def _grad_buffer(param, shape, like):
     return _empty(shape, like)
 
 
-def conv_weight_grad(x, dy, cout, upsample=1, pad_mode="zeros", with_bias=True, weight=None, bias=None):
+def conv_weight_grad(x, dy, cout, upsample=1, pad_mode="zeros", with_bias=True, weight=None, bias=None,
+                     dy_layout=(0, 0, 0)):
+    """dW, db of conv3x3(pad(upsample(x))); dy dense [n, cout, H, W] or, with dy_layout =
+    (pitch, plane, offset), the padded gradient buffer of the decoder dgrad."""
     x = _dev(x, "x")
     dy = _dev(dy, "dy")
     n, cin, h, w = (int(s) for s in x.shape)
     dw = _grad_buffer(weight, (cout, cin, 3, 3), x)
     db = _grad_buffer(bias, (cout,), x) if with_bias else None
     flops = 2 * n * h * upsample * w * upsample * cout * cin * 9
+    pitch, plane, off = dy_layout
     check(ops._timed(f"wgrad {cin}->{cout} {h * upsample}x{w * upsample}", flops, x.device,
-                     lambda: lib().ast_conv3x3_wgrad_f32(ptr(x), ptr(dy), ptr(dw), ptr(db), n, cin, h, w, cout,
-                                                         upsample, ops.PAD_MODES[pad_mode], _s(x))),
+                     lambda: lib().ast_conv3x3_wgrad_ex_f32(ptr(x), ptr(dy), ptr(dw), ptr(db), n, cin, h, w, cout,
+                                                            upsample, ops.PAD_MODES[pad_mode], pitch, plane, off,
+                                                            _s(x))),
           "conv3x3_wgrad")
     return dw, db
 
@@ -158,23 +163,21 @@ class DecoderConvFn(torch.autograd.Function):
         g = _dev(g, "grad")
         n, cout, H, W = out.shape
         cin = x.shape[1]
-        if ctx.relu:
-            dy = torch.empty_like(g)
-            check(lib().ast_relu_mask_f32(ptr(g), ptr(out), ptr(dy), g.numel(), _s(g)), "relu_mask")
-        else:
-            dy = g
+        # ReLU-masked output gradient, zero-padded by one pixel (pitch a multiple of 4 so the
+        # dgrad conv's vector gather applies): a same conv over it is the full padded-input grad
+        pitch = (W + 2 + 3) // 4 * 4
+        dyp = torch.empty((n, cout, H + 2, pitch), device=g.device, dtype=torch.float32)
+        check(lib().ast_grad_pad_f32(ptr(g), ptr(out) if ctx.relu else None, ptr(dyp), n * cout, H, W, pitch,
+                                     _s(g)), "grad_pad")
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dpin = conv_input_grad_same(dy, weight)
-            border = torch.empty((n, cin, 2 * (W + 2) + 2 * H), device=g.device, dtype=torch.float32)
-            wdet = _dev(weight.detach(), "weight")
-            check(lib().ast_conv3x3_dgrad_border_f32(ptr(dy), ptr(wdet), ptr(border), n, cout, cin, H, W, _s(g)),
-                  "dgrad_border")
+            dp = conv_input_grad_same(dyp, weight)          # [n, cin, H+2, pitch]
             dx = torch.empty_like(x)
-            check(lib().ast_pad_up_adjoint_f32(ptr(dpin), ptr(border), None, ptr(dx), n * cin, x.shape[2],
-                                               x.shape[3], ctx.upsample, _s(g)), "pad_up_adjoint")
+            check(lib().ast_pad_up_adjoint_f32(ptr(dp), ptr(dx), n * cin, x.shape[2], x.shape[3], ctx.upsample,
+                                               pitch, _s(g)), "pad_up_adjoint")
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            dw, db = conv_weight_grad(x, dy, cout, ctx.upsample, "reflect", ctx.has_bias, *ctx.param_ids)
+            dw, db = conv_weight_grad(x, dyp, cout, ctx.upsample, "reflect", ctx.has_bias, *ctx.param_ids,
+                                      dy_layout=(pitch, (H + 2) * pitch, pitch + 1))
         return dx, dw, db, None, None, None
 
 
@@ -295,22 +298,25 @@ class MVNHuberFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, y, weight):
         x, y = _dev(x, "x"), _dev(y, "y")
+        if x.shape != y.shape:
+            raise HipOpError(f"content loss: shape mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
         n, c = x.shape[:2]
         loss = _scalar(x)
-        check(lib().ast_mvn_huber_f32(ptr(x), ptr(y), n * c, x[0, 0].numel(), weight, None, ptr(loss), None, 0,
+        pstats = _empty((n * c, 6), x) if ctx.needs_input_grad[0] else None
+        check(lib().ast_mvn_huber_f32(ptr(x), ptr(y), n * c, x[0, 0].numel(), weight, ptr(loss), ptr(pstats),
                                       _s(x)), "mvn_huber")
-        ctx.save_for_backward(x, y)
+        ctx.save_for_backward(x, y, pstats)
         ctx.weight = weight
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        x, y = ctx.saved_tensors
+        x, y, pstats = ctx.saved_tensors
         g = _dev(g, "grad")
         n, c = x.shape[:2]
         dx = torch.empty_like(x)
-        check(lib().ast_mvn_huber_f32(ptr(x), ptr(y), n * c, x[0, 0].numel(), ctx.weight, ptr(g), None, ptr(dx), 0,
-                                      _s(x)), "mvn_huber")
+        check(lib().ast_mvn_huber_backward_f32(ptr(x), ptr(y), ptr(pstats), n * c, x[0, 0].numel(), ctx.weight,
+                                               ptr(g), ptr(dx), 0, _s(x)), "mvn_huber_backward")
         return dx, None, None
 
 
@@ -325,42 +331,45 @@ class StyleLossFn(torch.autograd.Function):
         if x.shape[:2] != y.shape[:2]:
             raise HipOpError("style loss: (N, C) mismatch")
         loss = _scalar(x)
-        _style_terms(x, y, weight, loss, None, None)
-        ctx.save_for_backward(x, y)
-        ctx.weight = weight
+        # with a gradient to come, the forward also keeps dG and the moment-term coefficients
+        # (all linear in grad_output), so the backward is one GEMM with grad_output as a scale
+        dg, ra, rb = _style_terms(x, y, weight, loss, want_grad=ctx.needs_input_grad[0])
+        ctx.save_for_backward(x, dg, ra, rb)
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        x, y = ctx.saved_tensors
+        x, dg, ra, rb = ctx.saved_tensors
+        b, c, h, w = x.shape
         dx = torch.empty_like(x)
-        _style_terms(x, y, ctx.weight, None, dx, _dev(g, "grad"))
+        check(lib().ast_gram_backward_f32(ptr(x), ptr(dg), ptr(dx), ptr(ra), ptr(rb), b, c, h * w, 1.0 / (c * h * w),
+                                          ptr(_dev(g, "grad")), 0, _s(x)), "gram_backward")
         return dx, None, None
 
 
-def _style_terms(x, y, weight, loss, dx, gscale, accumulate=False):
+def _style_terms(x, y, weight, loss, want_grad):
+    """Value of weight * compute_style_loss(x, y) added into `loss`; with want_grad also
+    (dG, row_a, row_b) of its gradient for grad_output = 1."""
     b, c, h, w = x.shape
     hw = h * w
     planes = b * c
     stats = _empty((planes, 4), x)
-    ra = _empty((planes,), x) if dx is not None else None
-    rb = _empty((planes,), x) if dx is not None else None
+    ra = _empty((planes,), x) if want_grad else None
+    rb = _empty((planes,), x) if want_grad else None
     L = lib()
     s = _s(x)
     if y.shape[2:] != x.shape[2:]:
         raise HipOpError("style loss: feature maps must have the same spatial size")
-    check(L.ast_style_moments_f32(ptr(x), ptr(y), planes, hw, weight, ptr(gscale), ptr(stats), ptr(loss), ptr(ra),
+    check(L.ast_style_moments_f32(ptr(x), ptr(y), planes, hw, weight, None, ptr(stats), ptr(loss), ptr(ra),
                                   ptr(rb), s), "style_moments")
     gx = _empty((b, c, c), x)
     gy = _empty((b, c, c), x)
     scale = 1.0 / (c * hw)
     check(L.ast_gram_f32(ptr(x), ptr(gx), b, c, hw, scale, s), "gram")
-    check(L.ast_gram_f32(ptr(y), ptr(gy), b, c, y[0, 0].numel(), 1.0 / (c * y[0, 0].numel()), s), "gram")
-    dg = _empty((b, c, c), x) if dx is not None else None
-    check(L.ast_gram_huber_f32(ptr(gx), ptr(gy), b * c * c, weight, ptr(gscale), ptr(loss), ptr(dg), s), "gram_huber")
-    if dx is not None:
-        check(L.ast_gram_backward_f32(ptr(x), ptr(dg), ptr(dx), ptr(ra), ptr(rb), b, c, hw, scale, None,
-                                      1 if accumulate else 0, s), "gram_backward")
+    check(L.ast_gram_f32(ptr(y), ptr(gy), b, c, hw, scale, s), "gram")
+    dg = _empty((b, c, c), x) if want_grad else None
+    check(L.ast_gram_huber_f32(ptr(gx), ptr(gy), b * c * c, weight, None, ptr(loss), ptr(dg), s), "gram_huber")
+    return dg, ra, rb
 
 
 class TVLossFn(torch.autograd.Function):

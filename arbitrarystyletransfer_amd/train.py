@@ -31,6 +31,13 @@ from . import models
 from .optim import FusedAdam
 
 STYLE_WEIGHTS = (1.0, 1.0, 1.0, 1.0, 0.75, 0.5)   # train.py:232-238 for the 6 loss-network layers
+LOSSNET_LAYERS = ["conv_1", "conv_3", "conv_5", "conv_9", "conv_13", "relu_15"]   # models.py:187
+# the loss network also emits relu_9 (= relu4_1, the AdaIN encoder output): with shared weights
+# one pass over content+style yields both the loss targets and the AdaIN inputs, and the pass over
+# the stylised batch yields enc(stylised) for the lf term.
+_TAPS = ["conv_1", "conv_3", "conv_5", "conv_9", "relu_9", "conv_13", "relu_15"]
+_LOSS_IDX = [0, 1, 2, 3, 5, 6]
+_RELU9 = 4
 
 
 def default_args(**kw):
@@ -46,8 +53,15 @@ class AdaINTrainer:
         self.device = torch.device(device or "cuda")
         self.net = (net or models.AdaINStyleTransfer()).to(self.device)
         self.net.encoder.requires_grad_(False).eval()
-        self.lossnet = (lossnet or models.PretrainedEncoder()).to(self.device).eval()
+        self.lossnet = (lossnet or models.PretrainedEncoder(_TAPS)).to(self.device).eval()
         self.lossnet.requires_grad_(False)
+        self.lossnet._content_layers = set(_TAPS)
+        # The AdaIN encoder is VGG19 to relu4_1 — the first 9 convs of the loss network. When the
+        # weights agree (the reference's setup: both pretrained VGG19), share them so one pass
+        # serves both; otherwise encode separately.
+        enc_convs, loss_convs = self.net.encoder.convs(), self.lossnet.convs()[:9]
+        self.shared = all(a.weight.shape == b.weight.shape and torch.equal(a.weight, b.weight) and
+                          torch.equal(a.bias, b.bias) for a, b in zip(enc_convs, loss_convs))
         self.params = [p for p in self.net.decoder.parameters()]
         self.optim = FusedAdam(self.params, lr=self.args.lr, betas=(0.9, 0.999), eps=1e-5, max_grad_norm=2.0,
                                error_if_nonfinite=True)
@@ -59,17 +73,21 @@ class AdaINTrainer:
     # ---- one step ----------------------------------------------------------------------------
     def compute_losses(self, content, style):
         a = self.args
+        b = content.shape[0]
         with torch.no_grad():
-            f_c, f_s = self.net.encode_pair(content, style)
+            taps = self.lossnet(content, style)                  # both batches in the same launches
+            if self.shared:
+                f_c, f_s = taps[_RELU9][:b], taps[_RELU9][b:]
+            else:
+                f_c, f_s = self.net.encode_pair(content, style)
             t = self.net.adain(f_c, f_s)
-            content_map = self.lossnet(content, style)          # both batches in the same launches
-            b = content.shape[0]
-            style_map = [m[b:] for m in content_map]
-            content_map = [m[:b] for m in content_map]
+            style_map = [taps[i][b:] for i in _LOSS_IDX]
+            content_map = [taps[i][:b] for i in _LOSS_IDX]
         stylized = self.net.decoder(t)
-        t_cs_map = self.lossnet(stylized)
+        s_taps = self.lossnet(stylized)
+        t_cs_map = [s_taps[i] for i in _LOSS_IDX]
         with torch.no_grad():
-            enc_stylized = self.net.encoder(stylized.detach())[0]
+            enc_stylized = s_taps[_RELU9].detach() if self.shared else self.net.encoder(stylized.detach())[0]
             lf_loss = L.content_mvn_loss(t, enc_stylized)
 
         content_terms = [L.content_mvn_loss(t_cs_map[i], content_map[i]) for i in range(len(t_cs_map))]
@@ -81,7 +99,7 @@ class AdaINTrainer:
         style_loss = torch.stack(style_terms).sum()
         loss = a.content_lam * content_loss + a.style_lam * style_loss + a.lf_lam * lf_loss + a.tv_lam * tv
         return {"loss": loss, "content_loss": content_loss, "style_loss": style_loss, "lf_loss": lf_loss,
-                "tv_loss": tv, "stylized": stylized}
+                "tv_loss": tv, "stylized": stylized, "t": t}
 
     def train_step(self, content, style, record=False):
         out = self.compute_losses(content, style)

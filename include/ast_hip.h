@@ -117,23 +117,29 @@ int ast_conv_act_backward_f32(const float* pre, const float* g_pre, const float*
 /* out = mask > 0 ? g : 0 (ReLU backward given the ReLU output). */
 int ast_relu_mask_f32(const float* g, const float* mask, float* out, long long n, void* stream);
 
-/* Reflect-pad dgrad border: gradient of the padded input on padded rows 0, h+1 and columns
- * 0, w+1 (dy [n, cout, h, w], w [cout, cin, 3, 3] unpacked); border [n, cin, 2(w+2)+2h]. */
-int ast_conv3x3_dgrad_border_f32(const float* dy, const float* w, float* border,
-                                 int n, int cout, int cin, int h, int w_, void* stream);
+/* Decoder dgrad, step 1: out_pad [planes, h+2, pitch] = zero-padded (mask > 0 ? g : 0)
+ * (g [planes, h, w]; mask = the layer's ReLU output, or NULL). A zero-padded same conv of
+ * out_pad with the transposed+flipped filter is then the FULL gradient of the padded input. */
+int ast_grad_pad_f32(const float* g, const float* mask, float* out_pad, long long planes,
+                     int h, int w, int pitch, void* stream);
 
-/* Adjoint of Upsample(x upsample, nearest) -> ReflectionPad2d(1): folds the padded-input
- * gradient (interior dp_interior [planes, h_in*up, w_in*up] + border) onto the source grid
- * dx [planes, h_in, w_in]; mask (optional, = the ReLU output that fed the layer): dx *= mask>0. */
-int ast_pad_up_adjoint_f32(const float* dp_interior, const float* border, const float* mask,
-                           float* dx, long long planes, int h_in, int w_in, int upsample,
-                           void* stream);
+/* Decoder dgrad, step 3: adjoint of Upsample(x upsample, nearest) -> ReflectionPad2d(1): folds
+ * the full padded-input gradient dp_full [planes, h_in*up+2, pitch] onto dx [planes, h_in, w_in]. */
+int ast_pad_up_adjoint_f32(const float* dp_full, float* dx, long long planes, int h_in, int w_in,
+                           int upsample, int pitch, void* stream);
 
 /* dw [cout, cin, 3, 3] = sum over images/pixels of dy x pad(upsample(x)) (zeroed here, MFMA
  * fp32, split over pixel tiles with fp32 atomics); db [cout] = sum of dy (optional). */
 int ast_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, float* db,
                           int n, int cin, int h_in, int w_in, int cout,
                           int upsample, int pad_mode, void* stream);
+
+/* Same with dy read through (pitch, plane stride, offset of element (0,0)) — e.g. the padded
+ * gradient buffer of ast_grad_pad_f32 (pitch, (h+2)*pitch, pitch+1). dy_pitch = 0: dense. */
+int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* db,
+                             int n, int cin, int h_in, int w_in, int cout, int upsample,
+                             int pad_mode, int dy_pitch, long long dy_plane, long long dy_offset,
+                             void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Losses (losses.py). Loss values are ADDED into the device scalar `loss` (may be NULL);
@@ -155,9 +161,15 @@ int ast_gram_backward_f32(const float* feat, const float* dgram, float* dfeat,
                           int accumulate, void* stream);
 
 /* compute_content_loss(mean_variance_norm(x), mean_variance_norm(y)) (losses.py:124-126,
- * models.py:64-68; train.py:225): loss += weight * mean(huber(mvn(x) - mvn(y))), dx = d/dx. */
+ * models.py:64-68; train.py:225): loss += weight * mean(huber(mvn(x) - mvn(y))). With pstats
+ * [planes, 6] (or NULL) it also keeps what the backward needs. */
 int ast_mvn_huber_f32(const float* x, const float* y, long long planes, long long hw, float weight,
-                      const float* gscale, float* loss, float* dx, int accumulate, void* stream);
+                      float* loss, float* pstats, void* stream);
+
+/* d/dx of the above (y constant), from the forward's pstats: one pass over x and y. */
+int ast_mvn_huber_backward_f32(const float* x, const float* y, const float* pstats, long long planes,
+                               long long hw, float weight, const float* gscale, float* dx,
+                               int accumulate, void* stream);
 
 /* compute_content_loss(x, y) = F.huber_loss(x, y) (delta 1, mean). */
 int ast_huber_f32(const float* x, const float* y, long long n, float weight, const float* gscale,
