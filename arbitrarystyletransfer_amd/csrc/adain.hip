@@ -118,6 +118,48 @@ __global__ __launch_bounds__(kThreads) void adain_kernel(const float* __restrict
   }
 }
 
+// Backward of adain_kernel. With c_hat = (c - mu_c)/sigma_c, (a, b) = (scale, shift) and g = dL/dy:
+//   dc = alpha*a*(g - mean(g) - c_hat*sum(g c_hat)/(N-1))/sigma_c + (1-alpha)*g
+//   da = alpha*sum(g c_hat), db = alpha*sum(g)  ->  (d mu_s, d sigma_s) by the swap rule
+//   ds = d mu_s / Ns + d sigma_s * (s - mu_s) / ((Ns-1) sigma_s)
+__global__ __launch_bounds__(kThreads) void adain_backward_kernel(const float* __restrict__ content,
+                                                                  const float* __restrict__ style,
+                                                                  const float* __restrict__ g, float* __restrict__ dc,
+                                                                  float* __restrict__ ds, int64_t hwc, int64_t hws,
+                                                                  float alpha, float beta, int swap) {
+  __shared__ float sh[kWaves];
+  const int64_t p = blockIdx.x;
+  const float* c = content + p * hwc;
+  const float* s = style + p * hws;
+  const float* gp = g + p * hwc;
+  float ms, ss, mc, sc;
+  plane_stats(s, hws, 1, 0.f, sh, ms, ss);
+  plane_stats(c, hwc, 1, 0.f, sh, mc, sc);
+  const float a = swap ? ms : ss;
+  float sg = 0.f, sgc = 0.f;
+  for (int64_t i = threadIdx.x; i < hwc; i += kThreads) {
+    const float gi = gp[i];
+    sg += gi;
+    sgc += gi * (c[i] - mc) / sc;
+  }
+  const float G = block_sum(sg, sh), GC = block_sum(sgc, sh);
+  if (dc) {
+    const float gmean = G / (float)hwc, gcz = GC / (float)(hwc - 1);
+    float* o = dc + p * hwc;
+    for (int64_t i = threadIdx.x; i < hwc; i += kThreads) {
+      const float z = (c[i] - mc) / sc;
+      o[i] = alpha * a * (gp[i] - gmean - z * gcz) / sc + beta * gp[i];
+    }
+  }
+  if (ds) {
+    const float da = alpha * GC, db = alpha * G;
+    const float dmu = swap ? da : db, dsd = swap ? db : da;
+    float* o = ds + p * hws;
+    for (int64_t i = threadIdx.x; i < hws; i += kThreads)
+      o[i] = dmu / (float)hws + dsd * (s[i] - ms) / ((float)(hws - 1) * ss);
+  }
+}
+
 __global__ void plane_normalize_kernel(const float* __restrict__ x, const float* __restrict__ mean,
                                        const float* __restrict__ sd, float* __restrict__ out, int64_t hw,
                                        int64_t total) {
@@ -148,6 +190,19 @@ int ast_adain_f32(const float* content, const float* style, float* out, int n, i
   const float a = (float)alpha, b = (float)(1.0 - alpha);
   hipLaunchKernelGGL(adain_kernel, dim3((unsigned)((int64_t)n * c)), dim3(kThreads), 0, (hipStream_t)stream, content,
                      style, out, (int64_t)hc * wc, (int64_t)hs * ws, a, b, swap_style_stats ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int ast_adain_backward_f32(const float* content, const float* style, const float* grad_out, float* d_content,
+                           float* d_style, int n, int c, int hc, int wc, int hs, int ws, double alpha,
+                           int swap_style_stats, void* stream) {
+  if (!content || !style || !grad_out) return AST_E_NULLPTR;
+  if (!d_content && !d_style) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hc <= 0 || wc <= 0 || hs <= 0 || ws <= 0) return AST_E_SHAPE;
+  const float a = (float)alpha, b = (float)(1.0 - alpha);
+  hipLaunchKernelGGL(adain_backward_kernel, dim3((unsigned)((int64_t)n * c)), dim3(kThreads), 0, (hipStream_t)stream,
+                     content, style, grad_out, d_content, d_style, (int64_t)hc * wc, (int64_t)hs * ws, a, b,
+                     swap_style_stats ? 1 : 0);
   return (int)hipGetLastError();
 }
 

@@ -225,6 +225,31 @@ class MeanVarianceNormFn(torch.autograd.Function):
         return dx
 
 
+class AdaINFn(torch.autograd.Function):
+    """AdaIN (models.py:43-51) + alpha blend (models.py:471), HIP forward and backward."""
+
+    @staticmethod
+    def forward(ctx, content, style, alpha, swap):
+        ctx.save_for_backward(content, style)
+        ctx.alpha, ctx.swap = alpha, swap
+        return ops.adain(content, style, alpha=alpha, swap_style_stats=swap)
+
+    @staticmethod
+    def backward(ctx, g):
+        content, style = ctx.saved_tensors
+        content, style = _dev(content, "content"), _dev(style, "style")
+        g = _dev(g, "grad")
+        n, c, hc, wc = content.shape
+        hs, ws = style.shape[2:]
+        dc = torch.empty_like(content) if ctx.needs_input_grad[0] else None
+        ds = torch.empty_like(style) if ctx.needs_input_grad[1] else None
+        if dc is None and ds is None:
+            return None, None, None, None
+        check(lib().ast_adain_backward_f32(ptr(content), ptr(style), ptr(g), ptr(dc), ptr(ds), n, c, hc, wc, hs, ws,
+                                           float(ctx.alpha), 1 if ctx.swap else 0, _s(g)), "adain_backward")
+        return dc, ds, None, None
+
+
 def channel_stats(x, unbiased=True, eps=0.0):
     if torch.is_grad_enabled() and x.requires_grad:
         return ChannelStatsFn.apply(x, unbiased, eps)

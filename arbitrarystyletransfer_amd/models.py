@@ -40,8 +40,7 @@ class AdaIN(nn.Module):
 
     def forward(self, content_map, style_map, alpha: float = 1.0):
         if torch.is_grad_enabled() and (content_map.requires_grad or style_map.requires_grad):
-            raise NotImplementedError("AdaIN backward is not implemented on HIP yet; the AdaIN training step "
-                                      "trains the decoder only (encode under torch.no_grad())")
+            return Fn.AdaINFn.apply(content_map, style_map, float(alpha), not self.canonical)
         return ops.adain(content_map, style_map, alpha=alpha, swap_style_stats=not self.canonical)
 
 

@@ -90,6 +90,11 @@ int ast_adain_f32(const float* content, const float* style, float* out,
                   int n, int c, int hc, int wc, int hs, int ws,
                   double alpha, int swap_style_stats, void* stream);
 
+/* Backward of ast_adain_f32: d_content and/or d_style (either may be NULL) from grad_out. */
+int ast_adain_backward_f32(const float* content, const float* style, const float* grad_out,
+                           float* d_content, float* d_style, int n, int c, int hc, int wc,
+                           int hs, int ws, double alpha, int swap_style_stats, void* stream);
+
 /* out = (x - mean[p]) / std[p] per plane (mean_variance_norm, models.py:64-68, given stats). */
 int ast_plane_normalize_f32(const float* x, const float* mean, const float* std, float* out,
                             long long planes, long long hw, void* stream);

@@ -165,6 +165,22 @@ def test_style_loss_vs_oracle(shape, hip_device):
     assert rel_inf(xd.grad, xr.grad) <= TOL
 
 
+@pytest.mark.parametrize("canonical,alpha,style_hw", [(False, 1.0, (6, 6)), (True, 0.6, (6, 6)), (False, 0.3, (9, 5))])
+def test_adain_backward(canonical, alpha, style_hw, hip_device):
+    c = rnd(61, (2, 8, 6, 6), 2.0, 0.5)
+    s = rnd(62, (2, 8) + style_hw, 1.5, 1.0)
+    g = rnd(63, (2, 8, 6, 6))
+    cr, sr = c.clone().requires_grad_(), s.clone().requires_grad_()
+    ref = R.alpha_blend((R.adain_canonical if canonical else R.adain)(cr, sr), cr, alpha)
+    (ref * g).sum().backward()
+    cd, sd = c.to(hip_device).requires_grad_(), s.to(hip_device).requires_grad_()
+    out = models.AdaIN(canonical=canonical)(cd, sd, alpha=alpha)
+    assert rel_inf(out, ref) <= 2e-5
+    (out * g.to(hip_device)).sum().backward()
+    assert rel_inf(cd.grad, cr.grad) <= TOL
+    assert rel_inf(sd.grad, sr.grad) <= TOL
+
+
 def test_channel_stats_backward(hip_device):
     x = rnd(31, (2, 5, 7, 9), 2.0, 1.0)
     gm, gs = rnd(32, (2, 5, 1, 1)), rnd(33, (2, 5, 1, 1))
