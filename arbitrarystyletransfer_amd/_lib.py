@@ -54,6 +54,12 @@ SIGNATURES = {
     "ast_grad_norm_f32": (_i, [_p, _i, _ll, _p, _f, _p, _p]),
     "ast_grad_scale_f32": (_i, [_p, _i, _ll, _p, _p]),
     "ast_adam_step_f32": (_i, [_p, _i, _ll, _p, _d, _d, _d, _d, _i, _p]),
+    "ast_mb_expand_dw": (_i, [_i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p,
+                              _i, _i, _p]),
+    "ast_mb_se_fold": (_i, [_i, _p, _i, _i, _ll, _p, _p, _i, _p, _p, _p, _i, _i, _i, _p, _p]),
+    "ast_mb_pw": (_i, [_i, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _i, _i, _p, _i, _p, _p]),
+    "ast_mb_conv3x3_dense": (_i, [_i, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
+    "ast_adain_bf16": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _d, _i, _p]),
 }
 
 ERRORS = {-1: "null pointer", -2: "bad shape", -3: "unsupported configuration"}

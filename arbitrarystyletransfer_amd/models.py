@@ -291,3 +291,189 @@ class AdaINStyleTransfer(nn.Module):
         f_c, f_s = self.encode_pair(content_img, style_img)
         t = self.adain(f_c, f_s, alpha=alpha)
         return self.decoder(t)
+
+
+# ------------------------------------------------------------------------------------------------
+# MobileNet-style variant: Encoder -> per-layer AdaIN -> ada_out ->
+# Decoder. Blocks are the DepthWiseConv/conv_3x3_bn mirrors of mobilenetv2.py (HIP forwards).
+# ------------------------------------------------------------------------------------------------
+from .mobilenetv2 import DTYPE_CODE, DepthWiseConv, SELayer, _make_divisible, act_dtype, check_inference  # noqa: E402,F401
+from .mobilenetv2 import _trace_io  # noqa: E402
+from .mobilenetv2 import conv_3x3_bn  # noqa: E402,F401
+from ._lib import HipOpError, check, lib, ptr, stream_ptr  # noqa: E402
+
+
+class Encoder(nn.Module):
+    """models.py:140-184: conv_3x3_bn + 14 DepthWiseConv blocks from conf.enc_conv_shapes; returns
+    the outputs of the blocks listed in out_layers. BatchNorm uses running statistics (eval)."""
+
+    def __init__(self, exporting=False, use_inst_norm=False):
+        super().__init__()
+        blocks = [conv_3x3_bn(enc_conv_shapes[0][0], enc_conv_shapes[0][1], enc_conv_shapes[0][2])]
+        for in_ch, out_ch, stride, kernel_size, expand_ratio in enc_conv_shapes[1:-1]:
+            blocks.append(DepthWiseConv(in_ch, out_ch, stride, expand_ratio, use_norm=True, kernel_size=kernel_size))
+        # models.py:153: the last block reuses the loop's final (in, out, stride) with EXPAND_RATIO
+        blocks.append(DepthWiseConv(in_ch, out_ch, stride, EXPAND_RATIO, use_norm=True))
+        self.mob_net = nn.ModuleList(blocks)
+
+    def forward(self, x, out_layers=[], auto_enc=False):
+        if auto_enc:
+            for layer in self.mob_net:
+                x = layer(x)
+            return x
+        outs = []
+        last = max(out_layers) if len(out_layers) else -1   # later blocks cannot change the result
+        for i, layer in enumerate(self.mob_net):
+            if i > last:
+                break
+            x = layer(x)
+            if i in out_layers:
+                outs.append(x)
+        return outs
+
+
+class DecoderBlock(nn.Module):
+    """models.py:242-272: DepthWiseConv (no BN), then optionally nearest Upsample x2 + ratio-1
+    DepthWiseConv (the upsample is fused into that block's depthwise gather)."""
+
+    def __init__(self, in_channels, out_channels, stride, kernel_size=3, upsample=False, expand_ratio=6):
+        super().__init__()
+        self._ref_pad = nn.ReflectionPad2d((1, 1, 1, 1))
+        self._conv = DepthWiseConv(in_channels, out_channels, stride, expand_ratio, use_norm=False,
+                                   kernel_size=kernel_size)
+        self._should_upsample = upsample
+        if self._should_upsample:
+            self._ref_out = nn.ReflectionPad2d((1, 1, 1, 1))
+            self._upsample_2 = DepthWiseConv(out_channels, out_channels, 1, 1, use_norm=False)
+            self._upsample_3 = nn.Upsample(scale_factor=2, mode="nearest")
+
+    def forward(self, x):
+        x = self._conv(x)
+        if self._should_upsample:
+            x = self._upsample_2.run(x, None, up=2)
+        return x
+
+
+class Decoder(nn.Module):
+    """models.py:274-320: 14 DecoderBlocks from conf.decoder_conv_shapes (upsample where the
+    channel count changes and i + 6 < 15, models.py:284), ReflectionPad + Conv(16->3, bias), and
+    Hardtanh(0, 1) only when exporting. Output in the parameters' dtype."""
+
+    def __init__(self, exporting=False):
+        super().__init__()
+        self.exporting = exporting
+        blocks = []
+        for i, conv_shape in enumerate(decoder_conv_shapes[:-1]):
+            should_upsample = conv_shape[0] != conv_shape[1] and i + 6 < len(decoder_conv_shapes)
+            blocks.append(DecoderBlock(conv_shape[0], conv_shape[1], conv_shape[2], upsample=should_upsample,
+                                       expand_ratio=conv_shape[4], kernel_size=conv_shape[3]))
+        self._decoder_blocks = nn.ModuleList(blocks)
+        self._ref_out = nn.ReflectionPad2d((1, 1, 1, 1))
+        self._img_out = nn.Conv2d(decoder_conv_shapes[-1][0], decoder_conv_shapes[-1][1], kernel_size=(3, 3))
+        self.last_act = nn.Hardtanh(0.0, 1.0)
+
+    def forward(self, x):
+        for block in self._decoder_blocks:
+            x = block(x)
+        return self._image_conv(x)
+
+    def _image_conv(self, x):
+        conv = self._img_out
+        check_inference(x, self)
+        dt = act_dtype(self)
+        if x.dtype != dt or x.device.type != "cuda" or x.dim() != 4 or x.shape[1] != conv.in_channels:
+            raise HipOpError(f"decoder output conv expects ({conv.in_channels}-channel NCHW {dt} on HIP), "
+                             f"got {tuple(x.shape)} {x.dtype} on {x.device}")
+        x = x.contiguous()
+        n, _, h, w = x.shape
+        stamp = (dt, x.device, ops.WEIGHTS_EPOCH[0], conv.weight._version, conv.bias._version,
+                 conv.weight.data_ptr())
+        if getattr(self, "_out_stamp", None) != stamp:
+            self._w = conv.weight.detach().float().contiguous()
+            self._b = conv.bias.detach().float().contiguous()
+            self._out_stamp = stamp
+        y = torch.empty((n, conv.out_channels, h, w), device=x.device, dtype=dt)
+        nbytes = x.numel() * x.element_size() + y.numel() * y.element_size()
+        _trace_io(nbytes)
+        check(ops._timed("mb dense3x3 out", -nbytes, x.device, lambda: lib().ast_mb_conv3x3_dense(
+            DTYPE_CODE[dt], DTYPE_CODE[dt], ptr(x), ptr(self._w), ptr(self._b), ptr(y), n, conv.in_channels,
+            conv.out_channels, h, w, 2 if self.exporting else 0, stream_ptr(x.device))), "decoder output conv")
+        return y
+
+
+class AutoEncoder(nn.Module):
+    """models.py:322-338: Encoder -> cat(layers 12, 14) -> ada_out -> Decoder."""
+
+    def __init__(self):
+        super().__init__()
+        self.encoder = Encoder(use_inst_norm=True)
+        self.ada_out = DepthWiseConv(enc_out_channels * 2, enc_out_channels, 1, EXPAND_RATIO, use_norm=False,
+                                     use_identity=False)
+        self.decoder = Decoder()
+
+    def load_live_init(self, enc_seed: int = 5, dec_seed: int = 6, ada_seed: int = 7):
+        synth.live_init_(self.encoder, enc_seed)
+        synth.live_init_(self.decoder, dec_seed)
+        synth.live_init_(self.ada_out, ada_seed)
+        return self
+
+    def forward(self, x):
+        enc_x = self.encoder(x, out_layers=enc_out_layers)
+        return self.decoder(self.ada_out(enc_x[0], enc_x[1]))
+
+
+class AST(nn.Module):
+    """The reference AST (models.py:393-582) with AdaIN as the stylisation op.
+
+    The reference class does not run (SyntaxError at models.py:459, missing
+    ada_att_2/ada_out); its AdaAttN op is off the hot path. This keeps the constructor and forward
+    signatures and return values (models.py:395,425,529-533) and the encode structure
+    (models.py:535-566) with AdaIN(content_i, style_i) at enc_out_layers. Inference only: BN uses
+    running statistics, so the reference's eval()/train() toggling in encode() is not needed.
+    """
+
+    def __init__(self, style_layers=[4, 7, 10, 12, 16], content_layers=[4, 7, 10, 12, 16], exporting=False):
+        super().__init__()
+        self._style_layers = style_layers
+        self._content_layers = content_layers
+        self._exporting = exporting
+        self._enc = Encoder(self._exporting)
+        self._dec = Decoder(self._exporting)
+        self._adain = AdaIN()
+        self.ada_out = DepthWiseConv(enc_out_channels * 2, enc_out_channels, 1, EXPAND_RATIO, use_norm=False,
+                                     use_identity=False)
+
+    def load_live_init(self, enc_seed: int = 5, dec_seed: int = 6, ada_seed: int = 7):
+        synth.live_init_(self._enc, enc_seed)
+        synth.live_init_(self._dec, dec_seed)
+        synth.live_init_(self.ada_out, ada_seed)
+        return self
+
+    def encode(self, content_img, style_img, detach=False, return_maps=False):
+        content_maps = self._enc(content_img, out_layers=enc_out_layers)
+        style_maps = self._enc(style_img, out_layers=enc_out_layers)
+        for m in content_maps:     # AdaIN reads content + style and writes its output
+            _trace_io(3 * m.numel() * m.element_size())
+        st1 = self._adain(content_maps[0], style_maps[0])
+        st2 = self._adain(content_maps[1], style_maps[1])
+        stylized_map = self.ada_out(st1, st2)
+        self._last_content_maps = content_maps
+        if return_maps:
+            return st1, st2, stylized_map
+        return stylized_map
+
+    def forward(self, content_img, style_img, alpha=1.0):
+        if not self._exporting:
+            t_return, _, t = self.encode(content_img, style_img, detach=True, return_maps=True)
+            c = self._last_content_maps            # == self._enc(content_img, enc_out_layers) in eval mode
+            content_map = self.ada_out(c[0], c[1])
+            if alpha != 1.0:
+                t = alpha * t + (1 - alpha) * content_map
+            org_out = self._dec(content_map)
+        else:
+            t = self.encode(content_img, style_img)
+        self._last_content_maps = None
+        t_cs = self._dec(t)
+        if self._exporting:
+            return t_cs
+        return t_cs, t_return, org_out

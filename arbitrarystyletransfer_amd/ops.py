@@ -176,6 +176,8 @@ def channel_stats(x: torch.Tensor, unbiased: bool = True, eps: float = 0.0):
 
 def adain(content: torch.Tensor, style: torch.Tensor, alpha: float = 1.0, swap_style_stats: bool = True):
     """AdaIN (models.py:43-51) fused with the alpha blend of models.py:471."""
+    if isinstance(content, torch.Tensor) and content.dtype == torch.bfloat16:
+        return adain_bf16(content, style, alpha, swap_style_stats)
     content = _dev(content, "content_map")
     style = _dev(style, "style_map")
     if content.dim() != 4 or style.dim() != 4 or content.shape[:2] != style.shape[:2]:
@@ -187,6 +189,32 @@ def adain(content: torch.Tensor, style: torch.Tensor, alpha: float = 1.0, swap_s
     check(_timed(f"adain {c}ch {hc}x{wc}", -nbytes, content.device, lambda: lib().ast_adain_f32(
         ptr(content), ptr(style), ptr(out), n, c, hc, wc, hs, ws, float(alpha), 1 if swap_style_stats else 0,
         stream_ptr(content.device))), "adain")
+    return out
+
+
+def _dev_typed(t: torch.Tensor, name: str, dtype: torch.dtype) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    if t.device.type != "cuda":
+        raise HipOpError(f"{name} is on {t.device}; arbitrarystyletransfer_amd runs on MI355X (HIP) devices only")
+    if t.dtype != dtype:
+        raise HipOpError(f"{name} must be {dtype}, got {t.dtype}")
+    return t.contiguous()
+
+
+def adain_bf16(content: torch.Tensor, style: torch.Tensor, alpha: float = 1.0, swap_style_stats: bool = True):
+    """AdaIN on bf16 maps (fp32 statistics and arithmetic, bf16 result)."""
+    content = _dev_typed(content, "content_map", torch.bfloat16)
+    style = _dev_typed(style, "style_map", torch.bfloat16)
+    if content.dim() != 4 or style.dim() != 4 or content.shape[:2] != style.shape[:2]:
+        raise HipOpError(f"AdaIN needs NCHW maps with equal (N, C): {tuple(content.shape)} vs {tuple(style.shape)}")
+    n, c, hc, wc = (int(s) for s in content.shape)
+    hs, ws = int(style.shape[2]), int(style.shape[3])
+    out = torch.empty_like(content)
+    nbytes = 2 * (2 * content.numel() + style.numel())
+    check(_timed(f"adain bf16 {c}ch {hc}x{wc}", -nbytes, content.device, lambda: lib().ast_adain_bf16(
+        ptr(content), ptr(style), ptr(out), n, c, hc, wc, hs, ws, float(alpha), 1 if swap_style_stats else 0,
+        stream_ptr(content.device))), "adain_bf16")
     return out
 
 

@@ -130,6 +130,41 @@ def vgg_decoder_weights(model_seed: int = 2):
     return out
 
 
+def live_init_(module, model_seed: int):
+    """Apply the live-init recipe to every Conv2d / BatchNorm2d / Linear of `module`, in
+    `named_modules()` order (leaf i uses streams layer_seed(model_seed, i) and +1).
+
+    Works on the reference's MobileNet modules (mobilenetv2.py:95-181, models.py:140-338) and on
+    this package's mirrors alike, because both have the same module tree. Returns `module`."""
+    import torch
+    import torch.nn as nn
+
+    i = 0
+    with torch.no_grad():
+        for _, m in module.named_modules():
+            s = layer_seed(model_seed, i)
+            if isinstance(m, nn.Conv2d):
+                kh, kw = m.kernel_size
+                assert kh == kw
+                w = conv_weight(s, m.out_channels, m.in_channels // m.groups, kh)
+                m.weight.copy_(torch.from_numpy(w))
+                if m.bias is not None:
+                    m.bias.copy_(torch.from_numpy(conv_bias(s + 1, m.out_channels)))
+            elif isinstance(m, nn.BatchNorm2d):
+                g, b, mu, var = bn_params(s, m.num_features)
+                m.weight.copy_(torch.from_numpy(g))
+                m.bias.copy_(torch.from_numpy(b))
+                m.running_mean.copy_(torch.from_numpy(mu))
+                m.running_var.copy_(torch.from_numpy(var))
+            elif isinstance(m, nn.Linear):
+                m.weight.copy_(torch.from_numpy(linear_weight(s, m.out_features, m.in_features)))
+                m.bias.copy_(torch.from_numpy(linear_bias(s + 1, m.out_features)))
+            else:
+                continue
+            i += 1
+    return module
+
+
 def checksum(a: np.ndarray):
     """Order-independent fingerprint used by the fixtures to pin this generator."""
     a64 = np.asarray(a, dtype=np.float64).ravel()

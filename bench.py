@@ -41,12 +41,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=8, help="images per GPU (config 2: 8)")
-    p.add_argument("--size", type=int, default=512)
+    p.add_argument("--batch", type=int, default=None, help="images per GPU (config 2: 8, config 5: 32)")
+    p.add_argument("--size", type=int, default=None, help="image side (config 2: 512, config 5: 1024)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(os.cpu_count(), OMP_NUM_THREADS or 16)")
-    p.add_argument("--mode", choices=["fwd", "train"], default="fwd",
-                   help="fwd: config 2 (the headline metric); train: config 3/4 AdaIN training step")
+    p.add_argument("--mode", choices=["fwd", "train", "mobilenet"], default="fwd",
+                   help="fwd: config 2 (the headline metric); train: config 3/4 AdaIN training step; "
+                        "mobilenet: config 5")
     return p.parse_args()
 
 
@@ -55,7 +56,7 @@ def train_bench(args, dev, rank, world):
     forward, loss network x3, losses, backward, all-reduce (N>1), clip + Adam."""
     from arbitrarystyletransfer_amd import dp
     from arbitrarystyletransfer_amd.train import AdaINTrainer, default_args
-    B, S = args.batch, args.size
+    B, S = args.batch or 16, args.size or 512
     arena = None
     trainer = AdaINTrainer(default_args(batch_size=B, image_size=S), device=dev)
     if world > 1:
@@ -108,6 +109,118 @@ def train_bench(args, dev, rank, world):
         print(json.dumps(result), flush=True)
 
 
+def mobilenet_bench(args, dev, rank, world):
+    """Config 5: MobileNet-style variant (Encoder x2 -> AdaIN@[12,14] -> ada_out -> Decoder,
+    exporting), bs=32/GPU at 1024x1024, bf16 storage with fp32 arithmetic. The roofline is HBM:
+    SURVEY.md §8d's block-fused minimum traffic (each block reads its input and writes its output
+    once) per step / step time, against 8 TB/s; `kernels` breaks the step down per kernel family."""
+    from arbitrarystyletransfer_amd import mobilenetv2
+    B, S = args.batch or 32, args.size or 1024
+    bf = torch.bfloat16
+    net = models.AST(exporting=True).load_live_init().eval().to(dev).to(bf)
+    content = torch.from_numpy(synth.image(821 + 2 * rank, (B, 3, S, S))).to(dev).to(bf)
+    style = torch.from_numpy(synth.image(822 + 2 * rank, (B, 3, S, S))).to(dev).to(bf)
+
+    def step():
+        with torch.no_grad():
+            return net(content, style)
+
+    mobilenetv2.IO_TRACE = []
+    out = step()
+    fused_min_bytes = sum(mobilenetv2.IO_TRACE)
+    mobilenetv2.IO_TRACE = None
+    for _ in range(max(0, args.warmup - 1)):
+        out = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    timer = ops.LaunchTimer()
+    t0 = time.perf_counter()
+    with timer:
+        for _ in range(args.steps):
+            out = step()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out.float()).all(), "non-finite output"
+    recs = timer.results()
+    fam = {}
+    for tag, nb, ms in recs:
+        key = tag.split(" ")[0] + " " + tag.split(" ")[1]
+        a = fam.setdefault(key, [0.0, 0.0, 0])
+        a[0] += -nb
+        a[1] += ms
+        a[2] += 1
+    kernels = {k: {"ms_per_step": v[1] / args.steps, "launches_per_step": v[2] // args.steps,
+                   "algorithmic_gbs": v[0] / (v[1] * 1e-3) / 1e9} for k, v in fam.items()}
+    step_s = elapsed / args.steps
+    achieved = fused_min_bytes / step_s / 1e9
+    ed = fam.get("mb expand_dw")
+    result = {
+        "metric": "stylised images/sec, MobileNet variant bs=32 1024x1024 bf16 (config 5)",
+        "value": B * world * args.steps / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (live-init MobileNet weights, U[0,1) images), resident in HBM",
+        "config": {"workload": f"config 5: MobileNet-style Encoder (content+style) -> AdaIN@[12,14] -> ada_out -> "
+                               f"Decoder(exporting), bs={B}/GPU {S}x{S}, bf16 storage / fp32 accumulate",
+                   "global_batch": B * world, "image_size": S, "parallelism": f"batch-sharded x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "whole step vs the block-fused minimum traffic (SURVEY §8d)",
+                     "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                     "traffic": None, "fused_min_gb_per_step": fused_min_bytes / 1e9,
+                     "expand_dw_gbs": (ed[0] / (ed[1] * 1e-3) / 1e9) if ed else None,
+                     "kernel_share_of_step": sum(m for _, _, m in recs) / args.steps / (step_s * 1e3)},
+        "kernels": kernels,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        threads = args.cpu_threads or min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+        result["cpu_baseline"] = cpu_baseline_mobilenet(S, args.cpu_seconds, threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def _cpu_model():
+    import platform
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return f"{cpu_model}, {platform.machine()}"
+
+
+def cpu_baseline_mobilenet(size, seconds, threads):
+    """The CPU oracle of the MobileNet variant (fp32: the reference has no bf16 CPU path)."""
+    from oracle import ref_cpu as R
+    torch.set_num_threads(threads)
+    sds = []
+    for m, seed in ((models.Encoder(), 5), (models.Decoder(), 6), (models.AutoEncoder().ada_out, 7)):
+        sds.append(synth.live_init_(m, seed).eval().state_dict())
+    c = torch.from_numpy(synth.image(821, (1, 3, size, size)))
+    s = torch.from_numpy(synth.image(822, (1, 3, size, size)))
+    with torch.no_grad():
+        R.mb_style_transfer(c[:, :, :64, :64], s[:, :, :64, :64], *sds)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            R.mb_style_transfer(c, s, *sds)
+            n += 1
+            dt = time.perf_counter() - t0
+            if dt >= seconds or n >= 64:
+                break
+    return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} content+style pair(s) of 1x3x{size}x{size}, MobileNet variant, fp32 torch CPU "
+                      f"({_cpu_model()}), {dt:.1f} s"}
+
+
 def cpu_baseline(size, seconds, threads):
     """Time the CPU oracle on single 512^2 pairs until `seconds` of work (at least one pair)."""
     from oracle import ref_cpu as R
@@ -152,13 +265,13 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    if args.mode == "train":
-        train_bench(args, dev, rank, world)
+    if args.mode in ("train", "mobilenet"):
+        (train_bench if args.mode == "train" else mobilenet_bench)(args, dev, rank, world)
         if world > 1:
             dist.destroy_process_group()
         return
 
-    B, S = args.batch, args.size
+    B, S = args.batch or 8, args.size or 512
     net = models.AdaINStyleTransfer().to(dev).eval()
     content = torch.from_numpy(synth.image(777 + 2 * rank, (B, 3, S, S))).to(dev)
     style = torch.from_numpy(synth.image(778 + 2 * rank, (B, 3, S, S))).to(dev)

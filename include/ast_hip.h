@@ -232,6 +232,51 @@ int ast_grad_scale_f32(const void* dev_table, int ntensors, long long nchunks, c
 int ast_adam_step_f32(const void* dev_table, int ntensors, long long nchunks, const float* state,
                       double lr, double beta1, double beta2, double eps, int step, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * MobileNet-style variant (config 5). dtype / dtype_in / dtype_out: 0 = fp32,
+ * 1 = bf16 storage (fp32 accumulate). All maps NCHW contiguous. BatchNorm (eval) is folded into
+ * the weights by the caller.
+ * ------------------------------------------------------------------------------------------ */
+
+/* DepthWiseConv.forward (mobilenetv2.py:153-165) up to the SE pool: the expand 1x1 conv
+ * (w1p != NULL: packed [round_up(hid,16)][cin_pad] in dtype, cin_pad a multiple of 32 (bf16) or 4
+ * (fp32), zero padded; b1 [hid]) + Hardswish, then the depthwise k x k conv (k 3|5, stride 1|2,
+ * reflect pad (k-1)/2; wdw [hid][k*k], bdw [hid]) + Hardswish, written to d [n][hid][ho][wo];
+ * pool [n][hid] receives the per-plane sums of d (zeroed here). w1p == NULL is the ratio-1 form
+ * (mobilenetv2.py:103-116): hid == cin, k == 3, and up == 2 applies DecoderBlock's nearest
+ * Upsample (models.py:264-266) to x first. x2 != NULL feeds channels [c1, cin) from a second
+ * tensor (the torch.cat before ada_out, models.py:335). */
+int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, int cin, int h, int w,
+                     int up, const void* w1p, const float* b1, int hid, int cin_pad,
+                     const float* wdw, const float* bdw, int k, int stride, void* d, float* pool,
+                     int ho, int wo, void* stream);
+
+/* SELayer (mobilenetv2.py:63-81) on the pooled sums (mean = pool / hw), folded into the pw-linear
+ * weights w2 [cout][hid]: wg[n][co][c] = w2[co][c] * gate[n][c], written as dtype
+ * [n][cout_pad][hid_pad] with zero padding. fc1w [red][hid], fc2w [hid][red]. */
+int ast_mb_se_fold(int dtype, const float* pool, int n, int hid, long long hw, const float* fc1w,
+                   const float* fc1b, int red, const float* fc2w, const float* fc2b, const float* w2,
+                   int cout, int cout_pad, int hid_pad, void* wg, void* stream);
+
+/* pw-linear conv: out[n][co] = sum_c wg[n*wg_stride + co*hid_pad + c] * d[n][c] + bias[co]
+ * (+ res[n][co], or res at (y/2, x/2) when res_up: the upsampled identity of models.py:266).
+ * hid_pad a multiple of 32, cout_pad a multiple of 16 (16..128, except 112). bias may be NULL. */
+int ast_mb_pw(int dtype, const void* d, int n, int hid, int hid_pad, int h, int w, const void* wg,
+              long long wg_stride, const float* bias, int cout, int cout_pad, const void* res,
+              int res_up, void* out, void* stream);
+
+/* Dense 3x3 reflect-pad convs of the variant: block 0 (conv_3x3_bn, mobilenetv2.py:38-43:
+ * cin 3 -> cout 16, no bias, act 1 = Hardswish, fp32 input) and the decoder output conv
+ * (models.py:300-316: cin 16 -> cout 3 + bias, fp32 output, act 2 = Hardtanh(0,1) when exporting,
+ * act 0 otherwise). wt [cout][cin][3][3]. */
+int ast_mb_conv3x3_dense(int dtype_in, int dtype_out, const void* x, const float* wt,
+                         const float* bias, void* y, int n, int cin, int cout, int h, int w, int act,
+                         void* stream);
+
+/* AdaIN (as ast_adain_f32) on bf16 maps, fp32 statistics. */
+int ast_adain_bf16(const void* content, const void* style, void* out, int n, int c, int hc, int wc,
+                   int hs, int ws, double alpha, int swap_style_stats, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

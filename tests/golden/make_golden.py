@@ -190,7 +190,68 @@ def main():
                         content_loss=cl.detach().numpy(), content_grad=content_grad.numpy(),
                         img=img.detach().numpy(), tv=tv.detach().numpy(), tv_grad=img.grad.numpy())
     train_step_golden(R, enc_wb, dec_wb)
+    mobilenet_golden(R)
     print("golden vectors written to", HERE)
+
+
+def _keep(a: torch.Tensor, limit: int = 20000):
+    """Full tensor if small, else its stride-2 spatial subsample (fixture size)."""
+    return a.numpy() if a.numel() <= limit else a[:, :, ::2, ::2].contiguous().numpy()
+
+
+def mobilenet_golden(R):
+    """MobileNet-style variant from the reference's own Encoder,
+    Decoder and AutoEncoder.ada_out modules (models.py:140-338, mobilenetv2.py) in eval mode with
+    the live-init weights: per-block maps, per-layer AdaIN, ada_out and the image (both
+    exporting settings)."""
+    enc = synth.live_init_(R["Encoder"](), 5).eval()
+    dec = synth.live_init_(R["Decoder"](), 6).eval()
+    ada = synth.live_init_(R["AutoEncoder"]().ada_out, 7).eval()
+    adain = R["AdaIN"]()
+    sums = {}
+    for tag, m in (("enc", enc), ("dec", dec), ("ada", ada)):
+        for k, v in m.state_dict().items():
+            if v.dtype.is_floating_point:
+                sums[f"{tag}:{k}"] = synth.checksum(v.numpy())
+    np.savez_compressed(os.path.join(HERE, "mb_weights_checksums.npz"), **sums)
+
+    def run(content, style, keep_blocks):
+        out = {}
+        with torch.no_grad():
+            h, maps = content, []
+            for i, layer in enumerate(enc.mob_net):            # Encoder.forward, models.py:177-182
+                h = layer(h)
+                maps.append(h)
+                out[f"enc_block{i}_chsum"] = h.double().sum(dim=(2, 3)).numpy()
+            sc = enc(style, out_layers=[12, 14])
+            cc = [maps[12], maps[14]]
+            a12, a14 = adain(cc[0], sc[0]), adain(cc[1], sc[1])
+            t = ada(torch.cat((a12, a14), dim=1))
+            h = t
+            for i, block in enumerate(dec._decoder_blocks):    # Decoder.forward, models.py:306-309
+                h = block(h)
+                if i in keep_blocks:
+                    out[f"dec_block{i}"] = _keep(h)
+                out[f"dec_block{i}_chsum"] = h.double().sum(dim=(2, 3)).numpy()
+            dec.exporting = False
+            y = dec(t)
+            dec.exporting = True
+            y_exp = dec(t)
+            dec.exporting = False
+        out.update(enc12=cc[0].numpy(), enc14=cc[1].numpy(),
+                   style12=sc[0].numpy(), style14=sc[1].numpy(), adain12=a12.numpy(), adain14=a14.numpy(),
+                   t=t.numpy(), out=y.numpy(), out_export=y_exp.numpy())
+        return out
+
+    # inputs are synth.image(seed, shape) (pinned by weights_checksums / test_oracle_golden)
+    for name, seeds, shape, keep_blocks in (("mb_path_64", (811, 812), (1, 3, 64, 64), (1, 2, 4, 7, 13)),
+                                            ("mb_path_128x96", (813, 814), (2, 3, 128, 96), (13,))):
+        r = run(torch.from_numpy(synth.image(seeds[0], shape)), torch.from_numpy(synth.image(seeds[1], shape)),
+                keep_blocks)
+        if shape[0] > 1:   # lean fixture: drop the intermediate maps the 64^2 fixture already pins
+            r = {k: v for k, v in r.items() if k not in ("style12", "style14", "adain12", "adain14")}
+            r["dec_block13"] = r["dec_block13"][:, :, ::2, ::2]
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), seeds=np.array(seeds), shape=np.array(shape), **r)
 
 
 def train_step_golden(R, enc_wb, dec_wb):
@@ -250,4 +311,8 @@ def train_step_golden(R, enc_wb, dec_wb):
 
 
 if __name__ == "__main__":
-    main()
+    if "--mobilenet" in sys.argv:
+        torch.manual_seed(0)
+        mobilenet_golden(load_reference())
+    else:
+        main()
