@@ -33,8 +33,8 @@ __device__ __forceinline__ float to_f(bf16 v) { return (float)v; }
 template <typename T>
 __device__ __forceinline__ T from_f(float v) { return (T)v; }
 
-// torch Hardswish: x * min(max(x + 3, 0), 6) / 6
-__device__ __forceinline__ float hswish(float v) { return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) / 6.f; }
+// torch Hardswish: x * min(max(x + 3, 0), 6) / 6 (here * (1/6): within 1 ulp, no IEEE divide sequence)
+__device__ __forceinline__ float hswish(float v) { return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f); }
 
 // Reflection-pad source index for i in [-(n-1), 2n-2]; clamped for out-of-tile garbage lanes.
 __device__ __forceinline__ int refl(int i, int n) {
@@ -56,14 +56,33 @@ struct Mma<bf16> {
     const bf16x8 fb = *reinterpret_cast<const bf16x8*>(b + r * ldb + kk);
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc, 0, 0, 0);
   }
+  // k = 16 tail (lane l: A[l&15][4(l>>4)+j], B[4(l>>4)+j][l&15]), so K pads to 16, not 32
+  __device__ static f32x4 step16(const bf16* a, const bf16* b, int lda, int ldb, int k0, f32x4 acc, int lane) {
+    typedef short s4 __attribute__((ext_vector_type(4)));
+    const int r = lane & 15, kk = k0 + 4 * (lane >> 4);
+    const s4 fa = *reinterpret_cast<const s4*>(a + r * lda + kk);
+    const s4 fb = *reinterpret_cast<const s4*>(b + r * ldb + kk);
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(fa, fb, acc, 0, 0, 0);
+  }
+  // acc += A . B over k in [0, kpad), kpad a multiple of 16
+  __device__ static f32x4 gemm(const bf16* a, const bf16* b, int lda, int ldb, int kpad, f32x4 acc, int lane) {
+    int k0 = 0;
+    for (; k0 + KS <= kpad; k0 += KS) acc = step(a, b, lda, ldb, k0, acc, lane);
+    if (k0 < kpad) acc = step16(a, b, lda, ldb, k0, acc, lane);
+    return acc;
+  }
 };
 template <>
 struct Mma<float> {
   static constexpr int KS = 4;
-  static constexpr int PAD = 1;
+  static constexpr int PAD = 4;   // keeps rows 16-byte aligned for the staging writes
   __device__ static f32x4 step(const float* a, const float* b, int lda, int ldb, int k0, f32x4 acc, int lane) {
     const int r = lane & 15, kk = k0 + (lane >> 4);
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a[r * lda + kk], b[r * ldb + kk], acc, 0, 0, 0);
+  }
+  __device__ static f32x4 gemm(const float* a, const float* b, int lda, int ldb, int kpad, f32x4 acc, int lane) {
+    for (int k0 = 0; k0 < kpad; k0 += KS) acc = step(a, b, lda, ldb, k0, acc, lane);
+    return acc;
   }
 };
 
@@ -107,11 +126,16 @@ struct EdGeom {
   static constexpr int IH = (TH - 1) * S + K;
   static constexpr int IW = (TW - 1) * S + K;
   static constexpr int NP = IH * IW;
-  static constexpr int HP = (NP + 15) / 16 * 16;
+  static constexpr int HP = (NP + 15) / 16 * 16;  // halo pixels as MFMA N tiles
   static constexpr int RP = TH / 2;         // output row pairs
   static constexpr int CG = 16 / RP;        // column groups per row pair
   static constexpr int CW = TW / CG;        // output columns per thread
   static_assert(RP * CG == 16 && CW * CG == TW && CW >= 1, "tile");
+  // Hidden-chunk LDS image hs[channel][row][col]: row pitch = 1 (mod 4), channel pitch = 1 (mod 8),
+  // so a half-wave's depthwise reads (2 channels x RP row pairs x CG column groups) fall in 32
+  // distinct banks for stride 1.
+  static constexpr int IWP = IW + ((1 - IW) % 4 + 4) % 4;
+  static constexpr int HPS = (IH * IWP + 7) / 8 * 8 + 1;
 };
 
 template <typename T, int K, int S, int TH, int TW>
@@ -119,8 +143,28 @@ __host__ __device__ constexpr size_t ed_lds_bytes(int cin_pad, bool expand) {
   using G = EdGeom<K, S, TH, TW>;
   const size_t xs = expand ? (size_t)G::HP * (cin_pad + Mma<T>::PAD) * sizeof(T) : 0;
   const size_t ws = expand ? (size_t)kChunk * (cin_pad + Mma<T>::PAD) * sizeof(T) : 0;
-  const size_t hs = (size_t)kChunk * G::HP * sizeof(float);
+  const size_t hs = (size_t)kChunk * G::HPS * sizeof(float);
   return xs + ws + hs;
+}
+
+template <typename T, int N>
+struct VecOf {
+  typedef T type __attribute__((ext_vector_type(N)));
+};
+
+// Store N consecutive outputs: one vector store when the run is whole and aligned.
+template <typename T, int N>
+__device__ __forceinline__ void store_run(T* o, const float* y, int count) {
+  if (count == N && ((uintptr_t)o % (sizeof(T) * N)) == 0) {
+    typename VecOf<T, N>::type v;
+#pragma unroll
+    for (int c = 0; c < N; ++c) v[c] = from_f<T>(y[c]);
+    *reinterpret_cast<typename VecOf<T, N>::type*>(o) = v;
+  } else {
+#pragma unroll
+    for (int c = 0; c < N; ++c)
+      if (c < count) o[c] = from_f<T>(y[c]);
+  }
 }
 
 template <typename T, int K, int S, int UP, bool EXPAND, int TH, int TW>
@@ -145,51 +189,93 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
   const T* x2 = reinterpret_cast<const T*>(a.x2);
   const int64_t hw = (int64_t)a.h * a.w;
 
-  auto src = [&](int c, int p) -> float {  // x[n][c] at halo pixel p (reflect pad in the dw grid)
+  // source offset (within a plane) of halo pixel p: reflect pad in the dw grid, then the upsample
+  auto src_off = [&](int p) -> int {
     int gy = refl(iy0 + p / G::IW, a.hd), gx = refl(ix0 + p % G::IW, a.wd);
     if (UP == 2) { gy >>= 1; gx >>= 1; }
-    const T* base = c < a.c1 ? x1 + ((int64_t)n * a.c1 + c) * hw
-                             : x2 + ((int64_t)n * (a.cin - a.c1) + (c - a.c1)) * hw;
-    return to_f(base[(int64_t)gy * a.w + gx]);
+    return gy * a.w + gx;
+  };
+  auto plane = [&](int c) -> const T* {
+    return c < a.c1 ? x1 + ((int64_t)n * a.c1 + c) * hw : x2 + ((int64_t)n * (a.cin - a.c1) + (c - a.c1)) * hw;
   };
 
-  if (EXPAND) {  // stage the x halo tile once, transposed: xs[p][c]
-    const int tot = a.cin_pad * G::HP;
-    for (int e = tid; e < tot; e += kThreads) {
-      const int c = e / G::HP, p = e - c * G::HP;
-      xs[p * ldx + c] = from_f<T>(c < a.cin && p < G::NP ? src(c, p) : 0.f);
+  if (EXPAND) {  // stage the x halo tile once, channel-minor: xs[p][c], one 16-byte write per channel group
+    constexpr int CV = 16 / sizeof(T);
+    const int groups = a.cin_pad / CV;
+    for (int e = tid; e < groups * G::HP; e += kThreads) {
+      const int g = e / G::HP, p = e - g * G::HP;  // lanes run along pixels: coalesced global loads
+      T v[CV];
+      if (p < G::NP) {
+        const int off = src_off(p);
+#pragma unroll
+        for (int j = 0; j < CV; ++j) {
+          const int c = g * CV + j;
+          v[j] = c < a.cin ? plane(c)[off] : from_f<T>(0.f);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < CV; ++j) v[j] = from_f<T>(0.f);
+      }
+      __builtin_memcpy(xs + p * ldx + g * CV, v, 16);
     }
   }
 
   // depthwise thread mapping: hidden channel hl of the chunk, output rows 2*rp, 2*rp+1, columns cg*CW..
   const int hl = tid >> 4, rp = (tid & 15) / G::CG, cg = (tid & 15) % G::CG;
   const int r0 = rp * 2, c0 = cg * G::CW;
+  constexpr int NT = G::HP / 16;              // MFMA N tiles (halo pixels / 16)
+  constexpr int TPW = (NT + 3) / 4;           // per wave
+  int hoff[TPW];                              // this lane's hs offset in each of its tiles (-1: padding)
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int p = (wave + 4 * i) * 16 + (lane & 15);
+    hoff[i] = p < G::NP ? (p / G::IW) * G::IWP + p % G::IW : -1;
+  }
+  // tiles wholly inside the output: no bounds checks, and every CW run is a vector-aligned store
+  const bool interior = oy0 + TH <= a.ho && ox0 + G::TW <= a.wo && (a.wo % G::CW) == 0;
+  const int64_t plane_o = (int64_t)a.ho * a.wo;
+  T* dbase = reinterpret_cast<T*>(a.d) + (int64_t)n * a.hid * plane_o + (int64_t)(oy0 + r0) * a.wo + ox0 + c0;
+  constexpr int CV = 16 / sizeof(T);
+
+  __shared__ float wdc[kChunk * K * K], bdc[kChunk], b1c[kChunk];  // this chunk's dw weights/biases
 
   for (int h0 = 0; h0 < a.hid; h0 += kChunk) {
+    for (int e = tid; e < kChunk * K * K; e += kThreads)
+      wdc[e] = h0 * K * K + e < a.hid * K * K ? a.wdw[h0 * K * K + e] : 0.f;
+    if (tid < kChunk) {
+      bdc[tid] = h0 + tid < a.hid ? a.bdw[h0 + tid] : 0.f;
+      b1c[tid] = EXPAND && h0 + tid < a.hid ? a.b1[h0 + tid] : 0.f;
+    }
     if (EXPAND) {
-      const T* w1 = reinterpret_cast<const T*>(a.w1);
-      for (int e = tid; e < kChunk * a.cin_pad; e += kThreads) {
-        const int r = e / a.cin_pad, c = e - r * a.cin_pad;
-        ws[r * ldx + c] = w1[(int64_t)(h0 + r) * a.cin_pad + c];
+      const T* w1 = reinterpret_cast<const T*>(a.w1) + (int64_t)h0 * a.cin_pad;
+      const int nv = a.cin_pad / CV;
+      for (int e = tid; e < kChunk * nv; e += kThreads) {
+        const int r = e / nv, v = e - r * nv;
+        *reinterpret_cast<uint4*>(ws + r * ldx + v * CV) = *reinterpret_cast<const uint4*>(w1 + r * a.cin_pad + v * CV);
       }
-      __syncthreads();  // xs (first chunk) and ws ready
+      __syncthreads();  // xs (first chunk), ws and the chunk's biases ready
       float bias[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int hc = h0 + 4 * (lane >> 4) + r;
-        bias[r] = hc < a.hid ? a.b1[hc] : 0.f;
-      }
-      for (int t = wave; t < G::HP / 16; t += kThreads / 64) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        for (int k0 = 0; k0 < a.cin_pad; k0 += Mma<T>::KS)
-          acc = Mma<T>::step(ws, xs + t * 16 * ldx, ldx, ldx, k0, acc, lane);
+      for (int r = 0; r < 4; ++r) bias[r] = b1c[4 * (lane >> 4) + r];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) hs[(4 * (lane >> 4) + r) * G::HP + t * 16 + (lane & 15)] = hswish(acc[r] + bias[r]);
+      for (int i = 0; i < TPW; ++i) {
+        const int t = wave + 4 * i;
+        if (t < NT) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          acc = Mma<T>::gemm(ws, xs + t * 16 * ldx, ldx, ldx, a.cin_pad, acc, lane);
+          if (hoff[i] >= 0) {
+            float* hp = hs + hoff[i] + 4 * (lane >> 4) * G::HPS;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hp[r * G::HPS] = hswish(acc[r] + bias[r]);
+          }
+        }
       }
     } else {
-      for (int e = tid; e < kChunk * G::NP; e += kThreads) {
-        const int r = e / G::NP, p = e - r * G::NP;
-        hs[r * G::HP + p] = h0 + r < a.hid ? src(h0 + r, p) : 0.f;
+      for (int p = tid; p < G::NP; p += kThreads) {
+        const int off = src_off(p);
+        float* hp = hs + (p / G::IW) * G::IWP + p % G::IW;
+#pragma unroll 4
+        for (int r = 0; r < kChunk; ++r) hp[r * G::HPS] = h0 + r < a.hid ? to_f(plane(h0 + r)[off]) : 0.f;
       }
     }
     __syncthreads();
@@ -199,19 +285,19 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
     if (hc < a.hid) {
       float wk[K * K];
 #pragma unroll
-      for (int i = 0; i < K * K; ++i) wk[i] = a.wdw[hc * K * K + i];
+      for (int i = 0; i < K * K; ++i) wk[i] = wdc[hl * K * K + i];
       float acc[2][G::CW];
 #pragma unroll
       for (int r = 0; r < 2; ++r)
 #pragma unroll
         for (int c = 0; c < G::CW; ++c) acc[r][c] = 0.f;
       constexpr int NCOL = (G::CW - 1) * S + K;
-      const float* hrow = hs + hl * G::HP + (r0 * S) * G::IW + c0 * S;
+      const float* hrow = hs + hl * G::HPS + (r0 * S) * G::IWP + c0 * S;
 #pragma unroll
       for (int j = 0; j < S + K; ++j) {
         float v[NCOL];
 #pragma unroll
-        for (int m = 0; m < NCOL; ++m) v[m] = hrow[j * G::IW + m];
+        for (int m = 0; m < NCOL; ++m) v[m] = hrow[j * G::IWP + m];
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
           const int ky = j - r * S;
@@ -223,22 +309,33 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
           }
         }
       }
-      const float bd = a.bdw[hc];
+      const float bd = bdc[hl];
       float psum = 0.f;
-      T* drow = reinterpret_cast<T*>(a.d) + ((int64_t)n * a.hid + hc) * a.ho * a.wo;
+      T* drow = dbase + (int64_t)hc * plane_o;
+      if (interior) {
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const int oy = oy0 + r0 + r;
-        if (oy >= a.ho) continue;
-        T* o = drow + (int64_t)oy * a.wo + ox0 + c0;
-        const int ncol = min(G::CW, a.wo - (ox0 + c0));
+        for (int r = 0; r < 2; ++r) {
+          typename VecOf<T, G::CW>::type v;
 #pragma unroll
-        for (int c = 0; c < G::CW; ++c) {
-          if (c < ncol) {
+          for (int c = 0; c < G::CW; ++c) {
             const float y = hswish(acc[r][c] + bd);
-            o[c] = from_f<T>(y);
             psum += y;
+            v[c] = from_f<T>(y);
           }
+          *reinterpret_cast<typename VecOf<T, G::CW>::type*>(drow + r * a.wo) = v;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          if (oy0 + r0 + r >= a.ho) continue;
+          const int ncol = min(G::CW, a.wo - (ox0 + c0));
+          float y[G::CW];
+#pragma unroll
+          for (int c = 0; c < G::CW; ++c) {
+            y[c] = hswish(acc[r][c] + bd);
+            if (c < ncol) psum += y[c];
+          }
+          if (ncol > 0) store_run<T, G::CW>(drow + r * a.wo, y, ncol);
         }
       }
 #pragma unroll
@@ -305,18 +402,49 @@ struct PwArgs {
 constexpr int kPwPx = 256;  // pixels per workgroup (4 waves x 64)
 constexpr int kPwK = 32;    // hidden channels per LDS stage
 
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// D is staged in its natural [channel][pixel] layout (16-byte writes, global loads coalesced along
+// pixels). bf16: the 16x16x32 B operand wants 8 channels of one pixel per lane, which the gfx950
+// transposed read ds_read_b64_tr_b16 delivers from that layout; the MFMA k order is permuted to
+// (4g..4g+3, 16+4g..16+4g+3) for lane group g (A uses the same order), so each half-wave's read
+// touches 8 consecutive rows, conflict-free with a row pitch of 16 (mod 128) elements.
 template <typename T, int MT>
 __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
-  constexpr int LD = kPwK + Mma<T>::PAD;
-  __shared__ __align__(16) T ds[kPwPx * LD];
-  __shared__ __align__(16) T ws[MT * 16 * LD];
+  constexpr bool BF = sizeof(T) == 2;
+  constexpr int LDP = kPwPx + (BF ? 16 : 4);     // D image row pitch (elements)
+  constexpr int LDW = kPwK + Mma<T>::PAD;        // weight image row pitch
+  constexpr int VEC = 16 / sizeof(T);            // elements per 16-byte vector
+  constexpr int NV = kPwK * kPwPx / VEC / kThreads;
+  constexpr int VPR = kPwPx / VEC;               // vectors per channel row
+  __shared__ __align__(16) T ds[kPwK * LDP];
+  __shared__ __align__(16) T ws[MT * 16 * LDW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = blockIdx.x / a.tiles;
   const int64_t p0 = (int64_t)(blockIdx.x % a.tiles) * kPwPx;
   const int64_t hw = (int64_t)a.h * a.w;
   const T* dn = reinterpret_cast<const T*>(a.d) + (int64_t)n * a.hid * hw;
   const T* wn = reinterpret_cast<const T*>(a.wg) + (int64_t)n * a.wg_stride;
-  const bool vec = (hw % 8) == 0 && p0 + kPwPx <= hw;
+  const bool vec = (hw % VEC) == 0 && p0 + kPwPx <= hw;
+
+  uint4 pre[NV];  // next chunk of D, prefetched into registers
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + i * kThreads, c = e / VPR, q = (e % VPR) * VEC;
+      if (vec) {
+        pre[i] = k0 + c < a.hid ? *reinterpret_cast<const uint4*>(dn + (int64_t)(k0 + c) * hw + p0 + q)
+                                : make_uint4(0, 0, 0, 0);
+      } else {
+        T tmp[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j)
+          tmp[j] = (k0 + c < a.hid && p0 + q + j < hw) ? dn[(int64_t)(k0 + c) * hw + p0 + q + j] : from_f<T>(0.f);
+        __builtin_memcpy(&pre[i], tmp, 16);
+      }
+    }
+  };
 
   f32x4 acc[MT][4];
 #pragma unroll
@@ -324,40 +452,53 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  fetch(0);
   for (int k0 = 0; k0 < a.hid_pad; k0 += kPwK) {
-    // D chunk [kPwK channels][256 px] -> ds[px][c]
-    if (vec) {
-      for (int e = tid; e < kPwK * (kPwPx / 8); e += kThreads) {
-        const int c = e / (kPwPx / 8), q = (e % (kPwPx / 8)) * 8;
-        float v[8];
-        if (k0 + c < a.hid) {
-          load8(dn + (int64_t)(k0 + c) * hw + p0 + q, v);
-        } else {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) v[i] = 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) ds[(q + i) * LD + c] = from_f<T>(v[i]);
-      }
-    } else {
-      for (int e = tid; e < kPwK * kPwPx; e += kThreads) {
-        const int c = e / kPwPx, q = e % kPwPx;
-        const bool ok = k0 + c < a.hid && p0 + q < hw;
-        ds[q * LD + c] = ok ? dn[(int64_t)(k0 + c) * hw + p0 + q] : from_f<T>(0.f);
-      }
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + i * kThreads, c = e / VPR, q = (e % VPR) * VEC;
+      *reinterpret_cast<uint4*>(ds + c * LDP + q) = pre[i];
     }
     for (int e = tid; e < MT * 16 * kPwK; e += kThreads) {
       const int r = e / kPwK, c = e % kPwK;
-      ws[r * LD + c] = wn[(int64_t)r * a.hid_pad + k0 + c];
+      ws[r * LDW + c] = wn[(int64_t)r * a.hid_pad + k0 + c];
     }
     __syncthreads();
+    if (k0 + kPwK < a.hid_pad) fetch(k0 + kPwK);  // in flight during the MFMAs
+    if constexpr (BF) {
+      const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+      bf16x8 bfr[4];
 #pragma unroll
-    for (int kk = 0; kk < kPwK; kk += Mma<T>::KS)
+      for (int t = 0; t < 4; ++t) {
+        const int col = wave * 64 + t * 16 + 4 * p;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds + (4 * g + q) * LDP + col));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds + (16 + 4 * g + q) * LDP + col));
+        bfr[t] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MT; ++m) {
+        const T* wr = ws + (m * 16 + (lane & 15)) * LDW + 4 * g;
+        const s16x4 lo = *reinterpret_cast<const s16x4*>(wr);
+        const s16x4 hi = *reinterpret_cast<const s16x4*>(wr + 16);
+        const bf16x8 afr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          acc[m][t] = Mma<T>::step(ws + m * 16 * LD, ds + (wave * 64 + t * 16) * LD, LD, LD, kk, acc[m][t], lane);
+        for (int t = 0; t < 4; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[t], acc[m][t], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < kPwK; ks += 4) {
+        const int kr = ks + (lane >> 4);
+        float bfr[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bfr[t] = ds[kr * LDP + wave * 64 + t * 16 + (lane & 15)];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const float afr = ws[(m * 16 + (lane & 15)) * LDW + kr];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(afr, bfr[t], acc[m][t], 0, 0, 0);
+        }
+      }
+    }
     __syncthreads();
   }
 
@@ -592,7 +733,7 @@ int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, i
   if (h * up <= p || w * up <= p) return AST_E_SHAPE;  // reflection pad needs pad < size
   const bool expand = w1p != nullptr;
   if (expand) {
-    const int ks = dtype == 1 ? 32 : 4;
+    const int ks = dtype == 1 ? 16 : 4;
     if (cin_pad < cin || cin_pad % ks != 0) return AST_E_SHAPE;
   } else if (hid != cin) {
     return AST_E_SHAPE;

@@ -218,7 +218,7 @@ class DepthWiseConv(nn.Module):
         else:
             i_pw1, i_dw, i_pw = convs
             w1, b1 = self._fold(i_pw1)
-            p.cin_pad = _round_up(self.inp, 32 if dt == torch.bfloat16 else 4)
+            p.cin_pad = _round_up(self.inp, 16 if dt == torch.bfloat16 else 4)
             w1p = torch.zeros((_round_up(hid, 16), p.cin_pad), device=device, dtype=torch.float32)
             w1p[:hid, :self.inp] = w1.view(hid, self.inp)
             p.w1p = w1p.to(dt).contiguous()

@@ -239,7 +239,7 @@ int ast_adam_step_f32(const void* dev_table, int ntensors, long long nchunks, co
  * ------------------------------------------------------------------------------------------ */
 
 /* DepthWiseConv.forward (mobilenetv2.py:153-165) up to the SE pool: the expand 1x1 conv
- * (w1p != NULL: packed [round_up(hid,16)][cin_pad] in dtype, cin_pad a multiple of 32 (bf16) or 4
+ * (w1p != NULL: packed [round_up(hid,16)][cin_pad] in dtype, cin_pad a multiple of 16 (bf16) or 4
  * (fp32), zero padded; b1 [hid]) + Hardswish, then the depthwise k x k conv (k 3|5, stride 1|2,
  * reflect pad (k-1)/2; wdw [hid][k*k], bdw [hid]) + Hardswish, written to d [n][hid][ho][wo];
  * pool [n][hid] receives the per-plane sums of d (zeroed here). w1p == NULL is the ratio-1 form
