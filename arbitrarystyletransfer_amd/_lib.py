@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (loads PyTorch's HIP runtime first, so the library binds to the same one)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libast_hip.so")
+LIB_PATH = os.environ.get("AST_HIP_LIB") or os.path.join(_HERE, "libast_hip.so")  # override: A/B kernel builds
 
 _c_float_p = ctypes.c_void_p
 _i = ctypes.c_int

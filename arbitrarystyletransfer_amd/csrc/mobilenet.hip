@@ -36,6 +36,11 @@ __device__ __forceinline__ T from_f(float v) { return (T)v; }
 // torch Hardswish: x * min(max(x + 3, 0), 6) / 6 (here * (1/6): within 1 ulp, no IEEE divide sequence)
 __device__ __forceinline__ float hswish(float v) { return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f); }
 
+// Workgroup barrier for LDS hand-offs only. __syncthreads() also fences global memory, i.e. waits
+// for every outstanding global load and store of the wave (vmcnt(0)): that would drain the dw
+// kernel's output stores and the pw kernel's in-flight prefetch at every chunk.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Reflection-pad source index for i in [-(n-1), 2n-2]; clamped for out-of-tile garbage lanes.
 __device__ __forceinline__ int refl(int i, int n) {
   i = i < 0 ? -i : i;
@@ -239,21 +244,57 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
 
   __shared__ float wdc[kChunk * K * K], bdc[kChunk], b1c[kChunk];  // this chunk's dw weights/biases
 
+  // The next chunk's weights are fetched into registers while this chunk computes.
+  constexpr int WSV = 4;                      // expand-weight vectors per thread (cin_pad <= 512)
+  constexpr int WDV = (kChunk * K * K + kThreads - 1) / kThreads;
+  const int nv = EXPAND ? a.cin_pad / CV : 0;
+  uint4 pw1[WSV];
+  float pwd[WDV], pb = 0.f;
+  // (a macro, not a lambda: a by-reference closure over these arrays sent them to scratch memory)
+#define ED_FETCH(H0)                                                                                       \
+  {                                                                                                        \
+    const int hh = (H0);                                                                                   \
+    if (EXPAND) {                                                                                          \
+      const T* w1 = reinterpret_cast<const T*>(a.w1) + (int64_t)hh * a.cin_pad;                            \
+      _Pragma("unroll") for (int i = 0; i < WSV; ++i) {                                                    \
+        const int e = tid + i * kThreads, r = e / max(nv, 1), v = e - r * nv;                              \
+        uint4 val = make_uint4(0, 0, 0, 0);                                                                \
+        if (e < kChunk * nv) val = *reinterpret_cast<const uint4*>(w1 + r * a.cin_pad + v * CV);           \
+        pw1[i] = val;                                                                                      \
+      }                                                                                                    \
+    }                                                                                                      \
+    _Pragma("unroll") for (int i = 0; i < WDV; ++i) {                                                      \
+      const int e = tid + i * kThreads;                                                                    \
+      float val = 0.f;                                                                                     \
+      if (e < kChunk * K * K && hh * K * K + e < a.hid * K * K) val = a.wdw[hh * K * K + e];               \
+      pwd[i] = val;                                                                                        \
+    }                                                                                                      \
+    float bv = 0.f;                                                                                        \
+    if (tid < kChunk) {                                                                                    \
+      if (hh + tid < a.hid) bv = a.bdw[hh + tid];                                                          \
+    } else if (EXPAND && tid < 2 * kChunk) {                                                               \
+      if (hh + tid - kChunk < a.hid) bv = a.b1[hh + tid - kChunk];                                         \
+    }                                                                                                      \
+    pb = bv;                                                                                               \
+  }
+  ED_FETCH(0);
+
   for (int h0 = 0; h0 < a.hid; h0 += kChunk) {
-    for (int e = tid; e < kChunk * K * K; e += kThreads)
-      wdc[e] = h0 * K * K + e < a.hid * K * K ? a.wdw[h0 * K * K + e] : 0.f;
-    if (tid < kChunk) {
-      bdc[tid] = h0 + tid < a.hid ? a.bdw[h0 + tid] : 0.f;
-      b1c[tid] = EXPAND && h0 + tid < a.hid ? a.b1[h0 + tid] : 0.f;
-    }
+#pragma unroll
+    for (int i = 0; i < WDV; ++i)
+      if (tid + i * kThreads < kChunk * K * K) wdc[tid + i * kThreads] = pwd[i];
+    if (tid < kChunk) bdc[tid] = pb;
+    else if (tid < 2 * kChunk) b1c[tid - kChunk] = pb;
     if (EXPAND) {
-      const T* w1 = reinterpret_cast<const T*>(a.w1) + (int64_t)h0 * a.cin_pad;
-      const int nv = a.cin_pad / CV;
-      for (int e = tid; e < kChunk * nv; e += kThreads) {
-        const int r = e / nv, v = e - r * nv;
-        *reinterpret_cast<uint4*>(ws + r * ldx + v * CV) = *reinterpret_cast<const uint4*>(w1 + r * a.cin_pad + v * CV);
+#pragma unroll
+      for (int i = 0; i < WSV; ++i) {
+        const int e = tid + i * kThreads, r = e / max(nv, 1), v = e - r * nv;
+        if (e < kChunk * nv) *reinterpret_cast<uint4*>(ws + r * ldx + v * CV) = pw1[i];
       }
-      __syncthreads();  // xs (first chunk), ws and the chunk's biases ready
+    }
+    lds_barrier();  // xs (first chunk), ws and the chunk's weights/biases ready
+    if (h0 + kChunk < a.hid) ED_FETCH(h0 + kChunk);
+    if (EXPAND) {
       float bias[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) bias[r] = b1c[4 * (lane >> 4) + r];
@@ -278,7 +319,7 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
         for (int r = 0; r < kChunk; ++r) hp[r * G::HPS] = h0 + r < a.hid ? to_f(plane(h0 + r)[off]) : 0.f;
       }
     }
-    __syncthreads();
+    lds_barrier();
 
     // depthwise kxk on the chunk
     const int hc = h0 + hl;
@@ -342,8 +383,9 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
       for (int o = 8; o > 0; o >>= 1) psum += __shfl_xor(psum, o, 64);
       if ((tid & 15) == 0) atomicAdd(a.pool + (int64_t)n * a.hid + hc, psum);
     }
-    __syncthreads();  // hs / ws reused by the next chunk
+    lds_barrier();  // hs / ws reused by the next chunk
   }
+#undef ED_FETCH
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -428,23 +470,36 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
   const T* wn = reinterpret_cast<const T*>(a.wg) + (int64_t)n * a.wg_stride;
   const bool vec = (hw % VEC) == 0 && p0 + kPwPx <= hw;
 
+  constexpr int WV = (MT * 16 * kPwK / VEC + kThreads - 1) / kThreads;
   uint4 pre[NV];  // next chunk of D, prefetched into registers
-  auto fetch = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int e = tid + i * kThreads, c = e / VPR, q = (e % VPR) * VEC;
-      if (vec) {
-        pre[i] = k0 + c < a.hid ? *reinterpret_cast<const uint4*>(dn + (int64_t)(k0 + c) * hw + p0 + q)
-                                : make_uint4(0, 0, 0, 0);
-      } else {
-        T tmp[VEC];
-#pragma unroll
-        for (int j = 0; j < VEC; ++j)
-          tmp[j] = (k0 + c < a.hid && p0 + q + j < hw) ? dn[(int64_t)(k0 + c) * hw + p0 + q + j] : from_f<T>(0.f);
-        __builtin_memcpy(&pre[i], tmp, 16);
-      }
-    }
-  };
+  uint4 prw[WV];  // and of the weights
+  // (a macro, not a lambda, and no address-taken temporaries: both sent these arrays to scratch)
+#define PW_FETCH(K0)                                                                                       \
+  {                                                                                                        \
+    const int kb = (K0);                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < NV; ++i) {                                                       \
+      const int e = tid + i * kThreads, c = e / VPR, q = (e % VPR) * VEC;                                  \
+      uint4 val = make_uint4(0, 0, 0, 0);                                                                  \
+      if (vec) {                                                                                           \
+        if (kb + c < a.hid) val = *reinterpret_cast<const uint4*>(dn + (int64_t)(kb + c) * hw + p0 + q);   \
+      } else {                                                                                             \
+        typename VecOf<T, VEC>::type tv;                                                                   \
+        _Pragma("unroll") for (int j = 0; j < VEC; ++j) {                                                  \
+          T x = from_f<T>(0.f);                                                                            \
+          if (kb + c < a.hid && p0 + q + j < hw) x = dn[(int64_t)(kb + c) * hw + p0 + q + j];              \
+          tv[j] = x;                                                                                       \
+        }                                                                                                  \
+        val = __builtin_bit_cast(uint4, tv);                                                               \
+      }                                                                                                    \
+      pre[i] = val;                                                                                        \
+    }                                                                                                      \
+    _Pragma("unroll") for (int i = 0; i < WV; ++i) {                                                       \
+      const int e = tid + i * kThreads, r = e / (kPwK / VEC), v = e % (kPwK / VEC);                        \
+      uint4 val = make_uint4(0, 0, 0, 0);                                                                  \
+      if (e < MT * 16 * kPwK / VEC) val = *reinterpret_cast<const uint4*>(wn + (int64_t)r * a.hid_pad + kb + v * VEC); \
+      prw[i] = val;                                                                                        \
+    }                                                                                                      \
+  }
 
   f32x4 acc[MT][4];
 #pragma unroll
@@ -452,19 +507,20 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  fetch(0);
+  PW_FETCH(0);
   for (int k0 = 0; k0 < a.hid_pad; k0 += kPwK) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = tid + i * kThreads, c = e / VPR, q = (e % VPR) * VEC;
       *reinterpret_cast<uint4*>(ds + c * LDP + q) = pre[i];
     }
-    for (int e = tid; e < MT * 16 * kPwK; e += kThreads) {
-      const int r = e / kPwK, c = e % kPwK;
-      ws[r * LDW + c] = wn[(int64_t)r * a.hid_pad + k0 + c];
+#pragma unroll
+    for (int i = 0; i < WV; ++i) {
+      const int e = tid + i * kThreads, r = e / (kPwK / VEC), v = e % (kPwK / VEC);
+      if (e < MT * 16 * kPwK / VEC) *reinterpret_cast<uint4*>(ws + r * LDW + v * VEC) = prw[i];
     }
-    __syncthreads();
-    if (k0 + kPwK < a.hid_pad) fetch(k0 + kPwK);  // in flight during the MFMAs
+    lds_barrier();
+    if (k0 + kPwK < a.hid_pad) PW_FETCH(k0 + kPwK);  // in flight during the MFMAs and across the barrier
     if constexpr (BF) {
       const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
       bf16x8 bfr[4];
@@ -499,7 +555,7 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 
   T* out = reinterpret_cast<T*>(a.out) + (int64_t)n * a.cout * hw;
@@ -529,6 +585,8 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
       }
     }
 }
+
+#undef PW_FETCH
 
 // ------------------------------------------------------------------------------------------------
 // dense 3x3 reflect conv with few channels (block 0: 3->16 + Hardswish; decoder out: 16->3 + bias)
