@@ -207,21 +207,23 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
   if (EXPAND) {  // stage the x halo tile once, channel-minor: xs[p][c], one 16-byte write per channel group
     constexpr int CV = 16 / sizeof(T);
     const int groups = a.cin_pad / CV;
-    for (int e = tid; e < groups * G::HP; e += kThreads) {
-      const int g = e / G::HP, p = e - g * G::HP;  // lanes run along pixels: coalesced global loads
-      T v[CV];
-      if (p < G::NP) {
-        const int off = src_off(p);
+    // channel c lives at xb1 + c*hw (c < c1) or xb2 + c*hw (c >= c1): wave-uniform selection
+    const T* xb1 = x1 + (int64_t)n * a.c1 * hw;
+    const T* xb2 = x2 + (int64_t)n * (a.cin - a.c1) * hw - (int64_t)a.c1 * hw;
+    for (int p = tid; p < G::HP; p += kThreads) {  // lanes run along pixels: coalesced global loads
+      const bool valid = p < G::NP;
+      const int off = valid ? src_off(p) : 0;
+      for (int g = 0; g < groups; ++g) {
+        typename VecOf<T, CV>::type v;
 #pragma unroll
         for (int j = 0; j < CV; ++j) {
           const int c = g * CV + j;
-          v[j] = c < a.cin ? plane(c)[off] : from_f<T>(0.f);
+          T x = from_f<T>(0.f);
+          if (c < a.cin && valid) x = (c < a.c1 ? xb1 : xb2)[(int64_t)c * hw + off];
+          v[j] = x;
         }
-      } else {
-#pragma unroll
-        for (int j = 0; j < CV; ++j) v[j] = from_f<T>(0.f);
+        *reinterpret_cast<typename VecOf<T, CV>::type*>(xs + p * ldx + g * CV) = v;
       }
-      __builtin_memcpy(xs + p * ldx + g * CV, v, 16);
     }
   }
 
