@@ -32,6 +32,7 @@ SIGNATURES = {
     "ast_adain_f32": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, ctypes.c_double, _i, _p]),
     "ast_plane_normalize_f32": (_i, [_p, _p, _p, _p, _ll, _ll, _p]),
     "ast_adain_backward_f32": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _d, _i, _p]),
+    "ast_adain_stats_f32": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _d, _i, _p]),
     "ast_conv3x3_pack_weights_ex_f32": (_i, [_p, _p, _i, _i, _i, _p, _p]),
     "ast_conv_act_backward_f32": (_i, [_p, _p, _p, _p, _p, _ll, _i, _i, _p]),
     "ast_relu_mask_f32": (_i, [_p, _p, _p, _ll, _p]),

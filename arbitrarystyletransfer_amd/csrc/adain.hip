@@ -160,6 +160,29 @@ __global__ __launch_bounds__(kThreads) void adain_backward_kernel(const float* _
   }
 }
 
+// AdaIN with the style statistics given (one-style-many-contents mode, SURVEY §8e: the style
+// owner computes (mean, std) once and broadcasts 2*C floats). Plane p = (n, c) uses
+// style_mean[(n * stride_n + c)], stride_n = 0 sharing one style across the batch.
+__global__ __launch_bounds__(kThreads) void adain_stats_kernel(const float* __restrict__ content,
+                                                               const float* __restrict__ smean,
+                                                               const float* __restrict__ sstd,
+                                                               float* __restrict__ out, int64_t hwc, int c,
+                                                               int stride_n, float alpha, float beta, int swap) {
+  __shared__ float sh[kWaves];
+  const int64_t p = blockIdx.x;
+  const int64_t si = (p / c) * stride_n + p % c;
+  const float ms = smean[si], ss = sstd[si];
+  const float* x = content + p * hwc;
+  float mc, sc;
+  plane_stats(x, hwc, 1, 0.f, sh, mc, sc);
+  const float scale = swap ? ms : ss, shift = swap ? ss : ms;
+  float* o = out + p * hwc;
+  for (int64_t i = threadIdx.x; i < hwc; i += kThreads) {
+    const float v = x[i];
+    o[i] = alpha * ((v - mc) / sc * scale + shift) + beta * v;
+  }
+}
+
 __global__ void plane_normalize_kernel(const float* __restrict__ x, const float* __restrict__ mean,
                                        const float* __restrict__ sd, float* __restrict__ out, int64_t hw,
                                        int64_t total) {
@@ -202,6 +225,18 @@ int ast_adain_backward_f32(const float* content, const float* style, const float
   const float a = (float)alpha, b = (float)(1.0 - alpha);
   hipLaunchKernelGGL(adain_backward_kernel, dim3((unsigned)((int64_t)n * c)), dim3(kThreads), 0, (hipStream_t)stream,
                      content, style, grad_out, d_content, d_style, (int64_t)hc * wc, (int64_t)hs * ws, a, b,
+                     swap_style_stats ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int ast_adain_stats_f32(const float* content, const float* style_mean, const float* style_std, float* out, int n,
+                        int c, int hc, int wc, int style_stride_n, double alpha, int swap_style_stats, void* stream) {
+  if (!content || !style_mean || !style_std || !out) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hc <= 0 || wc <= 0 || style_stride_n < 0) return AST_E_SHAPE;
+  if (style_stride_n != 0 && style_stride_n < c) return AST_E_SHAPE;
+  const float a = (float)alpha, b = (float)(1.0 - alpha);
+  hipLaunchKernelGGL(adain_stats_kernel, dim3((unsigned)((int64_t)n * c)), dim3(kThreads), 0, (hipStream_t)stream,
+                     content, style_mean, style_std, out, (int64_t)hc * wc, c, style_stride_n, a, b,
                      swap_style_stats ? 1 : 0);
   return (int)hipGetLastError();
 }

@@ -83,3 +83,14 @@ class FlatGradArena:
 
     def __call__(self, params=None):
         self.all_reduce()
+
+
+def broadcast_style_stats(style_mean, style_std, src: int = 0, group=None):
+    """One-style-many-contents mode: the rank owning the style image computed
+    its relu4_1 statistics (AdaINStyleTransfer.style_statistics); every rank receives them in one
+    broadcast of a packed [2, ...] tensor (2*512 fp32 = 4 KB). Other ranks pass tensors of the
+    same shape (contents ignored). Returns (mean, std) on every rank."""
+    packed = torch.stack([style_mean.reshape(-1), style_std.reshape(-1)]).contiguous()
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.broadcast(packed, src=src, group=group)
+    return packed[0].view_as(style_mean), packed[1].view_as(style_std)

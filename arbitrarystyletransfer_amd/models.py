@@ -292,6 +292,22 @@ class AdaINStyleTransfer(nn.Module):
         t = self.adain(f_c, f_s, alpha=alpha)
         return self.decoder(t)
 
+    # -- one style, many contents: the style owner encodes the style once and
+    #    broadcasts its relu4_1 statistics (dp.broadcast_style_stats, 2*512 floats) --------------
+    def style_statistics(self, style_img):
+        """(mean, std) of the style's relu4_1 features, each [N_style, 512]."""
+        f_s = self.encoder(style_img)[0]
+        m, s = channel_stats(f_s)
+        return m.flatten(1), s.flatten(1)
+
+    def stylize_with_stats(self, content_img, style_mean, style_std, alpha: float = 1.0):
+        """Stylise a content batch with given style statistics ([512] shared, or [N, 512])."""
+        if torch.is_grad_enabled() and (content_img.requires_grad or any(p.requires_grad for p in self.parameters())):
+            raise NotImplementedError("stylize_with_stats is inference-only; run it under torch.no_grad()")
+        f_c = self.encoder(content_img)[0]
+        t = ops.adain_stats(f_c, style_mean, style_std, alpha=alpha, swap_style_stats=not self.adain.canonical)
+        return self.decoder(t)
+
 
 # ------------------------------------------------------------------------------------------------
 # MobileNet-style variant (SURVEY.md §3.2, §8a A7-A9): Encoder -> per-layer AdaIN -> ada_out ->

@@ -192,6 +192,23 @@ def adain(content: torch.Tensor, style: torch.Tensor, alpha: float = 1.0, swap_s
     return out
 
 
+def adain_stats(content: torch.Tensor, style_mean: torch.Tensor, style_std: torch.Tensor, alpha: float = 1.0,
+                swap_style_stats: bool = True):
+    """AdaIN of `content` [N, C, H, W] against given style statistics: [C] (one style shared by
+    the batch) or [N, C] (any trailing 1-dims allowed), std unbiased as channel_stats."""
+    content = _dev(content, "content_map")
+    n, c, hc, wc = (int(s) for s in content.shape)
+    m = _dev(style_mean, "style_mean").reshape(-1)
+    s = _dev(style_std, "style_std").reshape(-1)
+    if m.numel() != s.numel() or m.numel() not in (c, n * c):
+        raise HipOpError(f"style statistics must have C={c} or N*C={n * c} entries, got {m.numel()}")
+    out = torch.empty_like(content)
+    check(lib().ast_adain_stats_f32(ptr(content), ptr(m), ptr(s), ptr(out), n, c, hc, wc,
+                                    0 if m.numel() == c else c, float(alpha), 1 if swap_style_stats else 0,
+                                    stream_ptr(content.device)), "adain_stats")
+    return out
+
+
 def _dev_typed(t: torch.Tensor, name: str, dtype: torch.dtype) -> torch.Tensor:
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name} must be a tensor")

@@ -90,6 +90,14 @@ int ast_adain_f32(const float* content, const float* style, float* out,
                   int n, int c, int hc, int wc, int hs, int ws,
                   double alpha, int swap_style_stats, void* stream);
 
+/* AdaIN with precomputed style statistics (one-style-many-contents mode, SURVEY §8e: the rank
+ * owning the style image computes them and broadcasts 2*C floats). style_mean/style_std are
+ * indexed [n * style_stride_n + c]; style_stride_n = 0 shares one style across the batch.
+ * std is the unbiased standard deviation (channel_stats, model_util.py:3-8). */
+int ast_adain_stats_f32(const float* content, const float* style_mean, const float* style_std,
+                        float* out, int n, int c, int hc, int wc, int style_stride_n, double alpha,
+                        int swap_style_stats, void* stream);
+
 /* Backward of ast_adain_f32: d_content and/or d_style (either may be NULL) from grad_out. */
 int ast_adain_backward_f32(const float* content, const float* style, const float* grad_out,
                            float* d_content, float* d_style, int n, int c, int hc, int wc,

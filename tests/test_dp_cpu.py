@@ -70,3 +70,44 @@ def test_dp_gradient_average_matches_single_process(tmp_path):
     g1, _ = _grads_for(content[2:], style[2:], dec_wb)
     ref = torch.cat([((x + y) / 2).reshape(-1) for x, y in zip(g0, g1)])
     np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-5, atol=1e-7 * float(ref.abs().max()))
+
+
+def _style_worker(rank, world, port, content, style, result_path):
+    """One style (owned by rank 0), contents sharded: rank 0 broadcasts relu4_1 style stats."""
+    from oracle import ref_cpu as R
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    enc = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_encoder_weights(1)[:9]]
+    dec = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_decoder_weights(2)]
+    with torch.no_grad():
+        if rank == 0:
+            m, s = R.channel_stats(R.vgg_encoder(style, enc)[0])
+            m, s = m.flatten(), s.flatten()
+        else:
+            m, s = torch.zeros(512), torch.full((512,), float("nan"))
+        m, s = dp.broadcast_style_stats(m, s, src=0)
+        a, b = dp.shard_range(content.shape[0], rank, world)
+        t = R.adain_from_stats(R.vgg_encoder(content[a:b], enc)[0], m, s)
+        y = R.vgg_decoder(t, dec)
+    torch.save({"m": m, "s": s, "y": y}, result_path + f".{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_style_stats_broadcast_one_style_many_contents(tmp_path):
+    from oracle import ref_cpu as R
+    content = torch.from_numpy(synth.image(911, (4, 3, 32, 32)))
+    style = torch.from_numpy(synth.image(912, (1, 3, 32, 32)))
+    path = str(tmp_path / "st")
+    mp.spawn(_style_worker, args=(2, _free_port(), content, style, path), nprocs=2, join=True)
+    r0 = torch.load(path + ".0", weights_only=True)
+    r1 = torch.load(path + ".1", weights_only=True)
+    assert torch.equal(r0["m"], r1["m"]) and torch.equal(r0["s"], r1["s"])
+    enc = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_encoder_weights(1)[:9]]
+    dec = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_decoder_weights(2)]
+    with torch.no_grad():
+        ref = R.style_transfer(content, style.expand(4, -1, -1, -1), enc, dec)
+    got = torch.cat([r0["y"], r1["y"]])
+    # CPU convs on different batch sizes pick different algorithms: fp32 reassociation only
+    np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=1e-4 * float(np.nanmax(np.abs(ref.numpy()))))

@@ -210,3 +210,21 @@ def test_style_transfer_512_batch8_vs_oracle(hip_device):
         ref = R.style_transfer(torch.from_numpy(c[i:i + 1]), torch.from_numpy(s[i:i + 1]), enc, dec)
         assert_e2e(y[i:i + 1], ref.numpy())
     assert torch.isfinite(y).all()
+
+
+def test_one_style_many_contents_stats(hip_device):
+    """stylize_with_stats (AdaIN from broadcastable style statistics) equals the
+    regular forward with the style replicated across the batch, and the kernel matches the oracle."""
+    net = models.AdaINStyleTransfer().to(hip_device)
+    c = torch.from_numpy(synth.image(931, (3, 3, 64, 96))).to(hip_device)
+    s = torch.from_numpy(synth.image(932, (1, 3, 64, 96))).to(hip_device)
+    with torch.no_grad():
+        m, sd = net.style_statistics(s)
+        y = net.stylize_with_stats(c, m[0], sd[0], alpha=0.8)
+        ref = net(c, s.expand(3, -1, -1, -1).contiguous(), alpha=0.8)
+        fc = net.encoder(c)[0]
+        t = ops.adain_stats(fc, m[0], sd[0], alpha=1.0)
+        t2 = ops.adain_stats(fc, m.expand(3, -1).contiguous(), sd.expand(3, -1).contiguous(), alpha=1.0)
+    assert rel_inf(y, ref) <= OP_TOL * 10
+    assert torch.equal(t, t2)
+    assert rel_inf(t, R.adain_from_stats(fc.cpu(), m[0].cpu(), sd[0].cpu())) <= OP_TOL
