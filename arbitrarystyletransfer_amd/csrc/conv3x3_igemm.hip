@@ -27,6 +27,7 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));  // register staging (HIP float4 arrays defeat SROA)
 
 constexpr int TW = 32;  // output tile width = one MFMA M-tile
 
@@ -97,7 +98,7 @@ __device__ __forceinline__ bool decode_block(int id, int ntiles, int groups, int
   return tile < ntiles;
 }
 
-template <int WM, int WN, int RM, int RN, int CK, int UP, bool SWAP>
+template <int WM, int WN, int RM, int RN, int CK, int UP, bool SWAP, bool NORM>
 __global__ __launch_bounds__(WM * WN * 64, 2) void conv3x3_f32_kernel(ConvArgs a) {
   using C = Cfg<WM, WN, RM, RN, CK, UP>;
   constexpr int NT = C::NT, TH = C::TH, BN = C::BN, SW = C::SW, SR = C::SR, RS = C::RS, QV = C::QV;
@@ -130,91 +131,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3x3_f32_kernel(ConvArgs a
   const float* __restrict__ xin =
       n < a.nsplit ? a.x + (int64_t)n * a.Cin * Hin * Win : a.x2 + (int64_t)(n - a.nsplit) * a.Cin * Hin * Win;
   const int plane_in = Hin * Win;
-
-  float4 ra[C::A_PER_T];
-  float4 rb[C::B_PER_T];
-
-  // ---- global -> registers (chunk starting at input channel cin0) ----
-  auto load_a_fast = [&](int cin0) {
-#pragma unroll
-    for (int i = 0; i < C::A_PER_T; ++i) {
-      const int e = tid + i * NT;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < C::A_ITEMS) {
-        const int q = e % (QV + 2);
-        const int cr = e / (QV + 2);
-        const int r = cr % SR, c = cr / SR;
-        const int cin = cin0 + c;
-        const int sy = src_index<UP>(sy0 + r, Hin, a.reflect);
-        if (cin < a.Cin && sy >= 0) {
-          const float* row = xin + cin * plane_in + sy * Win;
-          if (q < QV) {
-            v = *reinterpret_cast<const float4*>(row + sx0 + 4 * q);
-            if (a.in_mean) {
-              const float m = a.in_mean[cin], s = a.in_std[cin];
-              v.x = (v.x - m) / s; v.y = (v.y - m) / s; v.z = (v.z - m) / s; v.w = (v.w - m) / s;
-            }
-          } else {
-            const int sx = src_index<UP>(q == QV ? sx0 - 1 : sx0 + SW, Win, a.reflect);
-            if (sx >= 0) {
-              v.x = row[sx];
-              if (a.in_mean) v.x = (v.x - a.in_mean[cin]) / a.in_std[cin];
-            }
-          }
-        }
-      }
-      ra[i] = v;
-    }
-  };
-  auto store_a_fast = [&](float* as) {
-#pragma unroll
-    for (int i = 0; i < C::A_PER_T; ++i) {
-      const int e = tid + i * NT;
-      if (e < C::A_ITEMS) {
-        const int q = e % (QV + 2);
-        const int cr = e / (QV + 2);
-        float* row = as + cr * RS;
-        if (q < QV) *reinterpret_cast<float4*>(row + C::C0 + 4 * q) = ra[i];
-        else row[q == QV ? C::C0 - 1 : C::C0 + SW] = ra[i].x;
-      }
-    }
-  };
-  // Irregular tiles (right edge narrower than the tile, or W % 4 != 0): scalar gather into LDS.
-  auto fill_a_slow = [&](int cin0, float* as) {
-    for (int e = tid; e < C::S_ITEMS; e += NT) {
-      const int col = e % (SW + 2);
-      const int cr = e / (SW + 2);
-      const int r = cr % SR, c = cr / SR;
-      const int cin = cin0 + c;
-      const int sy = src_index<UP>(sy0 + r, Hin, a.reflect);
-      const int sx = src_index<UP>(sx0 - 1 + col, Win, a.reflect);
-      float v = 0.f;
-      if (cin < a.Cin && sy >= 0 && sx >= 0) {
-        v = xin[cin * plane_in + sy * Win + sx];
-        if (a.in_mean) v = (v - a.in_mean[cin]) / a.in_std[cin];
-      }
-      as[cr * RS + C::C0 - 1 + col] = v;
-    }
-  };
-  auto load_b = [&](int cin0) {
-#pragma unroll
-    for (int i = 0; i < C::B_PER_T; ++i) {
-      const int vi = tid + i * NT;
-      if (vi < C::B_VEC) {
-        const int f = vi * 4;
-        const int row = f / BN;  // = c*9 + tap
-        const int col = f - row * BN;
-        rb[i] = *reinterpret_cast<const float4*>(a.wp + (cin0 * 9 + row) * a.cout_pad + n0 + col);
-      }
-    }
-  };
-  auto store_b = [&](float* bs) {
-#pragma unroll
-    for (int i = 0; i < C::B_PER_T; ++i) {
-      const int vi = tid + i * NT;
-      if (vi < C::B_VEC) *reinterpret_cast<float4*>(bs + vi * 4) = rb[i];
-    }
-  };
+  const int nchunks = (a.Cin + CK - 1) / CK;
 
   f32x16 acc[RM][RN];
 #pragma unroll
@@ -231,61 +148,168 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3x3_f32_kernel(ConvArgs a
   const int abase = h * SR * RS;                       // lane half h reads channel 2kp+h
   const int bbase = h * 9 * BN + wn * RN * 32 + l32;
 
-  const int nchunks = (a.Cin + CK - 1) / CK;
+  // One K-chunk of MFMAs from LDS buffer `buf` (CK input channels x 9 taps).
+#define CONV_CHUNK_MFMA(buf)                                                                                 \
+  {                                                                                                         \
+    const float* as = As + (buf) * A_ELEMS + abase;                                                         \
+    const float* bs = Bs + (buf) * B_ELEMS + bbase;                                                         \
+    _Pragma("unroll") for (int ky = 0; ky < 3; ++ky) {                                                      \
+      _Pragma("unroll") for (int kx = 0; kx < 3; ++kx) {                                                    \
+        const int tap = ky * 3 + kx;                                                                        \
+        _Pragma("unroll") for (int kp = 0; kp < CK / 2; ++kp) {                                             \
+          float av[RM], bv[RN];                                                                             \
+          _Pragma("unroll") for (int i = 0; i < RM; ++i) {                                                  \
+            const int orow = wm * RM + i + ky - 1; /* -1 .. TH */                                           \
+            const int srow = (UP == 1) ? orow + 1 : (orow >> 1) + 1;                                        \
+            av[i] = as[(2 * kp * SR + srow) * RS + acol[kx]];                                               \
+          }                                                                                                 \
+          _Pragma("unroll") for (int j = 0; j < RN; ++j) bv[j] = bs[(2 * kp * 9 + tap) * BN + j * 32];      \
+          _Pragma("unroll") for (int i = 0; i < RM; ++i)                                                    \
+            _Pragma("unroll") for (int j = 0; j < RN; ++j)                                                  \
+              acc[i][j] = SWAP ? __builtin_amdgcn_mfma_f32_32x32x2f32(bv[j], av[i], acc[i][j], 0, 0, 0)     \
+                               : __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);    \
+        }                                                                                                   \
+      }                                                                                                     \
+    }                                                                                                       \
+  }
+
+  // Weight slab staging: B_VEC float4 per chunk; indices past the slab are clamped onto its last
+  // vector (duplicate loads and identical LDS writes, no branch).
+  constexpr int B_VEC = C::B_VEC, B_T = C::B_PER_T;
+  int boff[B_T];
+#pragma unroll
+  for (int i = 0; i < B_T; ++i) {
+    const int vi = min(tid + i * NT, B_VEC - 1), f = vi * 4, row = f / BN;
+    boff[i] = row * a.cout_pad + (f - row * BN);
+  }
+  const float* __restrict__ wbase = a.wp + n0;
+
   if (fast) {
-    load_a_fast(0);
-    store_a_fast(As);
-  } else {
-    fill_a_slow(0, As);
-  }
-  load_b(0);
-  store_b(Bs);
-  __syncthreads();
+    // Source-tile staging, branch-free: per-lane offsets computed once per tile; per chunk the
+    // channel base is a wave-uniform pointer. Interior items are float4 row pieces; each halo item
+    // is the aligned float4 that holds the (zero / reflect / replicate) halo column, one component kept.
+    constexpr int AI = CK * SR * QV, AI_T = (AI + NT - 1) / NT;
+    constexpr int AH = CK * SR * 2, AH_T = (AH + NT - 1) / NT;
+    int ai_g[AI_T], ai_l[AI_T], ai_c[AI_T];
+    bool ai_ok[AI_T];
+#pragma unroll
+    for (int i = 0; i < AI_T; ++i) {
+      const int e = min(tid + i * NT, AI - 1), q = e % QV, cr = e / QV, r = cr % SR, c = cr / SR;
+      const int sy = src_index<UP>(sy0 + r, Hin, a.reflect);
+      ai_ok[i] = sy >= 0;
+      ai_c[i] = c;
+      ai_g[i] = c * plane_in + max(sy, 0) * Win + sx0 + 4 * q;
+      ai_l[i] = cr * RS + C::C0 + 4 * q;
+    }
+    int ah_g[AH_T], ah_l[AH_T], ah_c[AH_T], ah_k[AH_T];  // ah_k: component 0..3, or -1 = zero
+#pragma unroll
+    for (int i = 0; i < AH_T; ++i) {
+      const int e = min(tid + i * NT, AH - 1), side = e & 1, cr = e >> 1, r = cr % SR, c = cr / SR;
+      const int sy = src_index<UP>(sy0 + r, Hin, a.reflect);
+      const int sx = src_index<UP>(side ? sx0 + SW : sx0 - 1, Win, a.reflect);
+      const bool ok = sy >= 0 && sx >= 0;
+      ah_k[i] = ok ? (sx & 3) : -1;
+      ah_c[i] = c;
+      ah_g[i] = c * plane_in + max(sy, 0) * Win + (ok ? (sx & ~3) : 0);
+      ah_l[i] = cr * RS + (side ? C::C0 + SW : C::C0 - 1);
+    }
+    f32x4 ra[AI_T], rh[AH_T], rb[B_T];
+    float nm[NORM ? AI_T : 1], ns[NORM ? AI_T : 1], hm[NORM ? AH_T : 1], hs[NORM ? AH_T : 1];
 
-  for (int kc = 0; kc < nchunks; ++kc) {
-    const int buf = kc & 1;
-    const bool more = kc + 1 < nchunks;
-    if (more) {
-      if (fast) load_a_fast((kc + 1) * CK);
-      load_b((kc + 1) * CK);
+    // issue every global load of chunk KC (no waits: the values are consumed by CONV_WRITE_CHUNK).
+    // (macros, not lambdas: a by-reference closure over the register arrays sends them to scratch)
+#define CONV_LOAD_CHUNK(KC)                                                                               \
+    {                                                                                                     \
+      const int cin0 = (KC) * CK;                                                                         \
+      const int cmax = a.Cin - 1 - cin0; /* chunk channels > cmax are zero */                             \
+      const float* __restrict__ xb = xin + (int64_t)cin0 * plane_in;                                      \
+      _Pragma("unroll") for (int i = 0; i < AI_T; ++i) {                                                  \
+        ra[i] = *reinterpret_cast<const f32x4*>(xb + (ai_c[i] <= cmax ? ai_g[i] : 0));                   \
+        if (NORM) {                                                                                       \
+          const int ch = cin0 + min(ai_c[i], cmax);                                                       \
+          nm[i] = a.in_mean[ch];                                                                          \
+          ns[i] = a.in_std[ch];                                                                           \
+        }                                                                                                 \
+      }                                                                                                   \
+      _Pragma("unroll") for (int i = 0; i < AH_T; ++i) {                                                  \
+        rh[i] = *reinterpret_cast<const f32x4*>(xb + (ah_c[i] <= cmax ? ah_g[i] : 0));                   \
+        if (NORM) {                                                                                       \
+          const int ch = cin0 + min(ah_c[i], cmax);                                                       \
+          hm[i] = a.in_mean[ch];                                                                          \
+          hs[i] = a.in_std[ch];                                                                           \
+        }                                                                                                 \
+      }                                                                                                   \
+      const float* __restrict__ wb = wbase + (int64_t)cin0 * 9 * a.cout_pad;                              \
+      _Pragma("unroll") for (int i = 0; i < B_T; ++i) rb[i] = *reinterpret_cast<const f32x4*>(wb + boff[i]); \
+    }
+#define CONV_WRITE_CHUNK(KC, BUF)                                                                         \
+    {                                                                                                     \
+      const int cmax = a.Cin - 1 - (KC) * CK;                                                             \
+      float* as = As + (BUF) * A_ELEMS;                                                                   \
+      _Pragma("unroll") for (int i = 0; i < AI_T; ++i) {                                                  \
+        f32x4 v = ra[i];                                                                                  \
+        if (NORM) v = (v - nm[i]) / ns[i];                                                                \
+        if (!(ai_ok[i] && ai_c[i] <= cmax)) v = f32x4{0.f, 0.f, 0.f, 0.f};                                \
+        *reinterpret_cast<f32x4*>(as + ai_l[i]) = v;                                                      \
+      }                                                                                                   \
+      _Pragma("unroll") for (int i = 0; i < AH_T; ++i) {                                                  \
+        const int k = ah_k[i];                                                                            \
+        const f32x4 q4 = rh[i];                                                                           \
+        float v = k == 0 ? q4.x : (k == 1 ? q4.y : (k == 2 ? q4.z : q4.w));                               \
+        if (NORM) v = (v - hm[i]) / hs[i];                                                                \
+        as[ah_l[i]] = (k >= 0 && ah_c[i] <= cmax) ? v : 0.f;                                              \
+      }                                                                                                   \
+      float* bs = Bs + (BUF) * B_ELEMS;                                                                   \
+      _Pragma("unroll") for (int i = 0; i < B_T; ++i)                                                     \
+        *reinterpret_cast<f32x4*>(bs + min(tid + i * NT, B_VEC - 1) * 4) = rb[i];                         \
     }
 
-    const float* as = As + buf * A_ELEMS + abase;
-    const float* bs = Bs + buf * B_ELEMS + bbase;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int tap = ky * 3 + kx;
-#pragma unroll
-        for (int kp = 0; kp < CK / 2; ++kp) {
-          float av[RM], bv[RN];
-#pragma unroll
-          for (int i = 0; i < RM; ++i) {
-            // output row (within tile) wm*RM+i, tap row ky -> source row in the LDS tile
-            const int orow = wm * RM + i + ky - 1;  // -1 .. TH
-            const int srow = (UP == 1) ? orow + 1 : (orow >> 1) + 1;
-            av[i] = as[(2 * kp * SR + srow) * RS + acol[kx]];
-          }
-#pragma unroll
-          for (int j = 0; j < RN; ++j) bv[j] = bs[(2 * kp * 9 + tap) * BN + j * 32];
-#pragma unroll
-          for (int i = 0; i < RM; ++i)
-#pragma unroll
-            for (int j = 0; j < RN; ++j)
-              acc[i][j] = SWAP ? __builtin_amdgcn_mfma_f32_32x32x2f32(bv[j], av[i], acc[i][j], 0, 0, 0)
-                               : __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
-        }
-      }
-    }
-    if (more) {
-      float* an = As + (buf ^ 1) * A_ELEMS;
-      if (fast) store_a_fast(an);
-      else fill_a_slow((kc + 1) * CK, an);
-      store_b(Bs + (buf ^ 1) * B_ELEMS);
-    }
+    CONV_LOAD_CHUNK(0);
+    CONV_WRITE_CHUNK(0, 0);
     __syncthreads();
+    for (int kc = 0; kc < nchunks; ++kc) {
+      const int buf = kc & 1;
+      const int kn = min(kc + 1, nchunks - 1);  // the last iteration re-loads into the idle buffer
+      CONV_LOAD_CHUNK(kn);
+      __builtin_amdgcn_sched_barrier(0);         // keep the loads ahead of the MFMAs
+      CONV_CHUNK_MFMA(buf);
+      __builtin_amdgcn_sched_barrier(0);
+      CONV_WRITE_CHUNK(kn, buf ^ 1);
+      __syncthreads();
+    }
+  } else {
+    // Irregular tiles (right edge narrower than the tile, or W % 4 != 0): scalar gather, no prefetch.
+    auto fill_a_slow = [&](int cin0, float* as) {
+      for (int e = tid; e < C::S_ITEMS; e += NT) {
+        const int col = e % (SW + 2);
+        const int cr = e / (SW + 2);
+        const int r = cr % SR, c = cr / SR;
+        const int cin = cin0 + c;
+        const int sy = src_index<UP>(sy0 + r, Hin, a.reflect);
+        const int sx = src_index<UP>(sx0 - 1 + col, Win, a.reflect);
+        float v = 0.f;
+        if (cin < a.Cin && sy >= 0 && sx >= 0) {
+          v = xin[cin * plane_in + sy * Win + sx];
+          if (NORM) v = (v - a.in_mean[cin]) / a.in_std[cin];
+        }
+        as[cr * RS + C::C0 - 1 + col] = v;
+      }
+    };
+    for (int kc = 0; kc < nchunks; ++kc) {
+      const int cin0 = kc * CK;
+      fill_a_slow(cin0, As);
+      const float* __restrict__ wb = wbase + (int64_t)cin0 * 9 * a.cout_pad;
+#pragma unroll
+      for (int i = 0; i < B_T; ++i)
+        *reinterpret_cast<float4*>(Bs + min(tid + i * NT, B_VEC - 1) * 4) = *reinterpret_cast<const float4*>(wb + boff[i]);
+      __syncthreads();
+      CONV_CHUNK_MFMA(0);
+      __syncthreads();
+    }
   }
+#undef CONV_CHUNK_MFMA
+#undef CONV_LOAD_CHUNK
+#undef CONV_WRITE_CHUNK
 
   // ---------------- epilogue ----------------
   const int H = a.H, W = a.W;
@@ -564,7 +588,7 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 inline int round_up(int a, int b) { return cdiv(a, b) * b; }
 
-template <int WM, int WN, int RM, int RN, int CK, int UP, bool SWAP>
+template <int WM, int WN, int RM, int RN, int CK, int UP, bool SWAP, bool NORM>
 int launch_one(const ConvArgs& a0, hipStream_t s) {
   using C = Cfg<WM, WN, RM, RN, CK, UP>;
   ConvArgs a = a0;
@@ -574,7 +598,7 @@ int launch_one(const ConvArgs& a0, hipStream_t s) {
   const int64_t ntiles = (int64_t)a.tiles_x * a.tiles_y * a.N;
   const int64_t nblk = (ntiles + 7) / 8 * 8 * cdiv(a.Cout, C::BN);
   if (nblk >= 0x7fffffff) return AST_E_SHAPE;
-  auto kern = conv3x3_f32_kernel<WM, WN, RM, RN, CK, UP, SWAP>;
+  auto kern = conv3x3_f32_kernel<WM, WN, RM, RN, CK, UP, SWAP, NORM>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
@@ -586,7 +610,9 @@ int launch_one(const ConvArgs& a0, hipStream_t s) {
 
 template <int WM, int WN, int RM, int RN, int CK, bool SWAP = false>
 int launch_cfg(const ConvArgs& a, hipStream_t s, int up) {
-  return up == 2 ? launch_one<WM, WN, RM, RN, CK, 2, SWAP>(a, s) : launch_one<WM, WN, RM, RN, CK, 1, SWAP>(a, s);
+  if (a.in_mean)  // ImageNet normalisation in the gather: conv_1 only (never upsampled)
+    return up == 2 ? launch_one<WM, WN, RM, RN, CK, 2, SWAP, true>(a, s) : launch_one<WM, WN, RM, RN, CK, 1, SWAP, true>(a, s);
+  return up == 2 ? launch_one<WM, WN, RM, RN, CK, 2, SWAP, false>(a, s) : launch_one<WM, WN, RM, RN, CK, 1, SWAP, false>(a, s);
 }
 
 template <int COUT>
