@@ -99,7 +99,7 @@ __device__ __forceinline__ bool decode_block(int id, int ntiles, int groups, int
 }
 
 template <int WM, int WN, int RM, int RN, int CK, int UP, bool SWAP, bool NORM>
-__global__ __launch_bounds__(WM * WN * 64, 2) void conv3x3_f32_kernel(ConvArgs a) {
+__global__ __launch_bounds__(WM * WN * 64, WM * WN >= 16 ? 1 : 2) void conv3x3_f32_kernel(ConvArgs a) {
   using C = Cfg<WM, WN, RM, RN, CK, UP>;
   constexpr int NT = C::NT, TH = C::TH, BN = C::BN, SW = C::SW, SR = C::SR, RS = C::RS, QV = C::QV;
   constexpr int A_ELEMS = C::A_ELEMS, B_ELEMS = C::B_ELEMS;
@@ -657,6 +657,8 @@ const CfgEntry kConfigs[] = {
     {launch_cfg<4, 2, 2, 2, 4, true>, 128, 8, 2, 0},   // 13: as 6
     {launch_cfg<4, 2, 4, 2, 4, true>, 128, 16, 4, 0},  // 14: as 8
     {launch_cfg<4, 1, 2, 2, 4, true>, 64, 8, 2, 0},    // 15: as 1
+    {launch_cfg<8, 2, 2, 2, 4>, 128, 16, 2, 0},        // 16: 16x32 px x 128 ch, CK 4, 16 waves (1 WG/CU)
+    {launch_cfg<8, 2, 2, 2, 4, true>, 128, 16, 2, 0},  // 17: as 16, swapped
 };
 constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 

@@ -18,6 +18,7 @@
 // Storage type T is float or __bf16; all arithmetic and accumulation is fp32.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "../../include/ast_hip.h"
 
 namespace {
@@ -391,6 +392,356 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// expand + depthwise, v2 (bf16 storage, stride 1): one barrier per hidden chunk
+// ------------------------------------------------------------------------------------------------
+// 512 threads, a TH x TW output tile of one image, hidden channels in chunks of 16. Per iteration c:
+//   (1) issue the global loads of chunk c+2's parameters (expand weights, dw weights, biases);
+//   (2) expand chunk c+1 on MFMA (operands swapped so each lane holds 4 consecutive halo pixels of
+//       one hidden channel), + bias, Hardswish, one 8-byte bf16 write into hidden image hs[(c+1)&1];
+//       ratio-1 blocks instead load chunk c+1's (upsampled, reflect-padded) input tile;
+//   (3) depthwise chunk c from hs[c&1]: each thread owns R output rows x 4 columns of one channel,
+//       reads its (R+K-1) x 8 input window with 8-byte LDS reads, fp32 FMAs, + bias, Hardswish,
+//       the SE pool partial sum (half-wave shuffle, one atomic per channel) and the bf16 D store;
+//   (4) write chunk c+2's parameters into the 3-slot LDS ring; one LDS-only barrier.
+// The hidden image holds bf16 (a bf16 model stores the expanded tensor in bf16); all arithmetic fp32.
+template <int K, int TH, int TW, int R, int NT_ = 512>
+struct Ed2Geom {
+  static constexpr int NT = NT_;
+  static constexpr int IH = TH + K - 1, IW = TW + K - 1;
+  static constexpr int IWE = (IW + 3) / 4 * 4;     // halo row length of the expand enumeration
+  static constexpr int NPE = IH * IWE;
+  static constexpr int HP = (NPE + 15) / 16 * 16;  // expand pixels, MFMA tiles of 16
+  static constexpr int NTILE = HP / 16;
+  static constexpr int TPC = (TH / R) * (TW / 4);  // threads per channel
+  static_assert(NT / TPC == 16, "16 hidden channels per chunk (the MFMA N)");
+  static_assert(TPC == 32 || TPC == 64, "a channel's threads are one half-wave or wave (pool shuffle)");
+  // image pitch: the next row group's rows land 16 banks away (conflict-free 8-byte reads)
+  static constexpr int pitch() {
+    for (int p = IWE; p <= IWE + 16; p += 4)
+      if ((R * p) % 64 == 32) return p;
+    return IWE;
+  }
+  static constexpr int IWP = pitch();
+  static constexpr int CHP = (IH * IWP + 63) / 64 * 64 + 4;  // channel pitch (bf16), = 4 mod 64
+  static constexpr int NR = R + K - 1;                      // input rows per thread
+  static constexpr int KKP = (K * K + 3) / 4 * 4;           // dw weight row pitch (floats)
+  static constexpr int WIN = 16 * IH * IWE;                 // ratio-1 input elements per chunk
+};
+
+struct Ed2Slot {  // byte offsets inside one parameter slot
+  int w1, wd, b1, bd, bytes;
+};
+template <int K>
+__host__ __device__ constexpr Ed2Slot ed2_slot(int ldx, bool expand) {
+  const int w1b = expand ? 16 * ldx * 2 : 0;
+  const int wdb = 16 * ((K * K + 3) / 4 * 4) * 4;
+  return Ed2Slot{0, w1b, w1b + wdb, w1b + wdb + 64, w1b + wdb + 128};
+}
+
+template <int K, int TH, int TW, int R, int NT = 512>
+__host__ __device__ constexpr size_t ed2_lds_bytes(int cin_pad, bool expand, int hid) {
+  using G = Ed2Geom<K, TH, TW, R, NT>;
+  const int ldx = cin_pad + 8;
+  const size_t xs = expand ? (size_t)G::HP * ldx * 2 : 0;
+  const size_t hs = (size_t)2 * 16 * G::CHP * 2;
+  return xs + hs + 4 * (size_t)ed2_slot<K>(ldx, expand).bytes + (size_t)(hid + 3) / 4 * 16;
+}
+
+#ifndef ED2_PHASE_FENCE
+#define ED2_PHASE_FENCE 1
+#endif
+#ifndef ED2_SKIP
+#define ED2_SKIP 0  // experiment builds: 1 = no D store, 2 = no depthwise FMAs, 4 = no expand
+#endif
+template <int K, int UP, bool EXPAND, int TH, int TW, int R, int NT_>
+__global__ __launch_bounds__(NT_, 4) void expand_dw2_kernel(EdArgs a) {  // 4 waves per SIMD: <= 128 VGPRs
+  using G = Ed2Geom<K, TH, TW, R, NT_>;
+  constexpr int NT = G::NT, IH = G::IH, IW = G::IW, IWE = G::IWE, IWP = G::IWP, CHP = G::CHP, NR = G::NR;
+  constexpr int P = (K - 1) / 2;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int ldx = a.cin_pad + 8;
+  const Ed2Slot sl = ed2_slot<K>(ldx, EXPAND);
+  bf16* xs = reinterpret_cast<bf16*>(smem);
+  bf16* hs = xs + (EXPAND ? G::HP * ldx : 0);                               // [2][16][CHP]
+  unsigned char* ring = reinterpret_cast<unsigned char*>(hs + 2 * 16 * CHP);  // [4][slot]
+  float* pool_s = reinterpret_cast<float*>(ring + 4 * sl.bytes);              // [hid] this tile's SE sums
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // image index fastest: co-resident workgroups belong to different images, so their SE-pool
+  // atomics (one per channel per tile) do not pile onto the same few addresses
+  const int n = blockIdx.x % a.n;
+  int b = blockIdx.x / a.n;
+  const int tx = b % a.tiles_x;
+  const int ty = b / a.tiles_x;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 - P, ix0 = ox0 - P;
+  const int64_t hw = (int64_t)a.h * a.w;
+  const bf16* x1 = reinterpret_cast<const bf16*>(a.x1);
+  const bf16* x2 = reinterpret_cast<const bf16*>(a.x2);
+  const int nch = (a.hid + 15) / 16;
+
+  // source offset (within a plane) of halo position (row, col) of the dw input grid
+  auto src_off = [&](int row, int col) -> int {
+    int gy = refl(iy0 + row, a.hd), gx = refl(ix0 + min(col, IW - 1), a.wd);
+    if (UP == 2) { gy >>= 1; gx >>= 1; }
+    return gy * a.w + gx;
+  };
+
+  if (EXPAND) {  // x halo tile, channel-minor: xs[p][c]; p = row * IWE + col (cols >= IW duplicate IW-1)
+    const bf16* xb1 = x1 + (int64_t)n * a.c1 * hw;
+    const bf16* xb2 = x2 + (int64_t)n * (a.cin - a.c1) * hw - (int64_t)a.c1 * hw;
+    for (int p = tid; p < G::HP; p += NT) {
+      const int pp = min(p, G::NPE - 1);
+      const int off = src_off(pp / IWE, pp % IWE);
+      for (int g0 = 0; g0 < a.cin_pad; g0 += 32) {  // 32 loads in flight, then four 16-byte writes
+        bf16x8 v[4];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          const int c = g0 + j;
+          bf16 xv = (bf16)0.f;
+          if (c < a.cin) xv = (c < a.c1 ? xb1 : xb2)[(int64_t)c * hw + off];
+          v[j >> 3][j & 7] = xv;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (g0 + 8 * q < a.cin_pad) *reinterpret_cast<bf16x8*>(xs + p * ldx + g0 + 8 * q) = v[q];
+      }
+    }
+  }
+
+  // ---- parameter ring: global -> registers (set B) -> registers (set A, one iteration later, so
+  // the loads' latency is a whole iteration) -> LDS slot cc % 4 ----
+  constexpr int NSLOT = 4;
+  const int nw1 = EXPAND ? 16 * a.cin_pad / 8 : 0;  // uint4 vectors of expand weights per chunk
+  uint4 pw1B = make_uint4(0, 0, 0, 0), pw1A = pw1B;
+  float pwdB = 0.f, pbB = 0.f, pwdA = 0.f, pbA = 0.f;
+#define ED2_FETCH(CC)                                                                                      \
+  {                                                                                                        \
+    const int h0 = (CC) * 16;                                                                              \
+    if (EXPAND && tid < nw1) {                                                                             \
+      const int r = tid / (a.cin_pad / 8), v = tid % (a.cin_pad / 8);                                      \
+      pw1B = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.w1) + (int64_t)(h0 + r) * a.cin_pad + v * 8); \
+    }                                                                                                      \
+    pwdB = 0.f;                                                                                            \
+    if (tid < 16 * K * K && h0 + tid / (K * K) < a.hid) pwdB = a.wdw[(int64_t)h0 * K * K + tid];           \
+    pbB = 0.f;                                                                                             \
+    if (tid < 16) {                                                                                        \
+      if (h0 + tid < a.hid) pbB = a.bdw[h0 + tid];                                                         \
+    } else if (EXPAND && tid < 32) {                                                                       \
+      if (h0 + tid - 16 < a.hid) pbB = a.b1[h0 + tid - 16];                                                \
+    }                                                                                                      \
+  }
+#define ED2_STASH(CC)                                                                                      \
+  {                                                                                                        \
+    unsigned char* s_ = ring + ((CC) % NSLOT) * sl.bytes;                                                  \
+    if (EXPAND && tid < nw1) {                                                                             \
+      const int r = tid / (a.cin_pad / 8), v = tid % (a.cin_pad / 8);                                      \
+      *reinterpret_cast<uint4*>(s_ + sl.w1 + (r * ldx + v * 8) * 2) = pw1A;                                \
+    }                                                                                                      \
+    if (tid < 16 * K * K) reinterpret_cast<float*>(s_ + sl.wd)[(tid / (K * K)) * G::KKP + tid % (K * K)] = pwdA; \
+    if (tid < 16) reinterpret_cast<float*>(s_ + sl.bd)[tid] = pbA;                                         \
+    else if (EXPAND && tid < 32) reinterpret_cast<float*>(s_ + sl.b1)[tid - 16] = pbA;                     \
+  }
+#define ED2_ROTATE() { pw1A = pw1B; pwdA = pwdB; pbA = pbB; }
+
+  // ratio-1 blocks: the chunk's input tile straight from x (upsample + reflect), two register sets
+  // like the parameters (loads consumed one iteration after they are issued)
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  constexpr int WP = EXPAND ? 1 : (G::WIN / 2 + NT - 1) / NT;  // bf16 pairs per thread
+  bf16x2 rinB[WP], rinA[WP];
+#define ED2_LOAD_IN(CC)                                                                                    \
+  if constexpr (!EXPAND) {                                                                                 \
+    _Pragma("unroll") for (int i = 0; i < WP; ++i) {                                                       \
+      const int e = 2 * (tid + i * NT);                                                                    \
+      bf16x2 v = {(bf16)0.f, (bf16)0.f};                                                                   \
+      if (e < G::WIN) {                                                                                    \
+        const int ch_ = e / (IH * IWE), rem = e % (IH * IWE), row = rem / IWE, col = rem % IWE;            \
+        const int c_ = (CC) * 16 + ch_;                                                                    \
+        if (c_ < a.hid) {                                                                                  \
+          const bf16* xp = x1 + ((int64_t)n * a.cin + c_) * hw;                                            \
+          v[0] = xp[src_off(row, col)];                                                                    \
+          v[1] = xp[src_off(row, col + 1)];                                                                \
+        }                                                                                                  \
+      }                                                                                                    \
+      rinB[i] = v;                                                                                         \
+    }                                                                                                      \
+  }
+#define ED2_STORE_IN(BUF)                                                                                  \
+  if constexpr (!EXPAND) {                                                                                 \
+    _Pragma("unroll") for (int i = 0; i < WP; ++i) {                                                       \
+      const int e = 2 * (tid + i * NT);                                                                    \
+      if (e < G::WIN) {                                                                                    \
+        const int ch_ = e / (IH * IWE), rem = e % (IH * IWE);                                              \
+        *reinterpret_cast<bf16x2*>(hs + (BUF) * 16 * CHP + ch_ * CHP + (rem / IWE) * IWP + rem % IWE) = rinA[i]; \
+      }                                                                                                    \
+    }                                                                                                      \
+  }
+#define ED2_ROTATE_IN() if constexpr (!EXPAND) { _Pragma("unroll") for (int i = 0; i < WP; ++i) rinA[i] = rinB[i]; }
+
+  // expand chunk cc into hs[buf]: this wave's tiles t = wave, wave + 8, ... (K outer, tiles inner,
+  // so every tile's LDS operand reads of one K step are in flight together)
+  constexpr int TPW = (G::NTILE + NT / 64 - 1) / (NT / 64);
+  auto expand = [&](int cc, int buf) {
+    if constexpr (EXPAND && !(ED2_SKIP & 4)) {
+      const unsigned char* s_ = ring + (cc % NSLOT) * sl.bytes;
+      const bf16* ws = reinterpret_cast<const bf16*>(s_ + sl.w1);
+      const float bias = reinterpret_cast<const float*>(s_ + sl.b1)[lane & 15];
+      f32x4 acc[TPW];
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int r = lane & 15;
+      int k0 = 0;
+      for (; k0 + 32 <= a.cin_pad; k0 += 32) {
+        const int kk = k0 + 8 * (lane >> 4);
+        const bf16x8 fb = *reinterpret_cast<const bf16x8*>(ws + r * ldx + kk);
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+          const int t = wave + (NT / 64) * i;
+          if (t < G::NTILE) {
+            const bf16x8 fa = *reinterpret_cast<const bf16x8*>(xs + (t * 16 + r) * ldx + kk);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[i], 0, 0, 0);
+          }
+        }
+      }
+      if (k0 < a.cin_pad) {  // k = 16 tail
+        typedef short s4 __attribute__((ext_vector_type(4)));
+        const int kk = k0 + 4 * (lane >> 4);
+        const s4 fb = *reinterpret_cast<const s4*>(ws + r * ldx + kk);
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+          const int t = wave + (NT / 64) * i;
+          if (t < G::NTILE) {
+            const s4 fa = *reinterpret_cast<const s4*>(xs + (t * 16 + r) * ldx + kk);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(fa, fb, acc[i], 0, 0, 0);
+          }
+        }
+      }
+      bf16* hb = hs + buf * 16 * CHP + (lane & 15) * CHP;
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        const int t = wave + (NT / 64) * i;
+        const int p0 = t * 16 + 4 * (lane >> 4);
+        if (t < G::NTILE && p0 < G::NPE) {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          bf16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = (bf16)hswish(acc[i][j] + bias);
+          *reinterpret_cast<bf16x4*>(hb + (p0 / IWE) * IWP + p0 % IWE) = o;
+        }
+      }
+    }
+  };
+
+  // depthwise mapping: channel ch of the chunk, output rows rg*R.., columns sg*4..
+  constexpr int TPC = G::TPC;
+  const int ch = tid / TPC, rg = (tid % TPC) >> 3, sg = tid & 7;
+  const int r0 = rg * R, c0 = sg * 4;
+  const int64_t plane_o = (int64_t)a.ho * a.wo;
+  const bool interior = oy0 + TH <= a.ho && ox0 + TW <= a.wo && (a.wo % 4) == 0;
+  bf16* dbase = reinterpret_cast<bf16*>(a.d) + (int64_t)n * a.hid * plane_o + (int64_t)(oy0 + r0) * a.wo + ox0 + c0;
+
+  auto depthwise = [&](int cc, int buf) {
+    const int hc = cc * 16 + ch;
+    if (hc >= a.hid) return;  // uniform per half-wave
+    const unsigned char* s = ring + (cc % NSLOT) * sl.bytes;
+    const float* wd = reinterpret_cast<const float*>(s + sl.wd) + ch * G::KKP;  // LDS broadcast reads
+    const float bd = reinterpret_cast<const float*>(s + sl.bd)[ch];
+    const bf16* hrow = hs + buf * 16 * CHP + ch * CHP + r0 * IWP + c0;
+    typedef short s16x4v __attribute__((ext_vector_type(4)));
+    float acc[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const s16x4v lo = *reinterpret_cast<const s16x4v*>(hrow + j * IWP);
+      const s16x4v hi = *reinterpret_cast<const s16x4v*>(hrow + j * IWP + 4);
+      float v[8];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        v[m] = __builtin_bit_cast(float, (unsigned)(unsigned short)lo[m] << 16);
+        v[m + 4] = __builtin_bit_cast(float, (unsigned)(unsigned short)hi[m] << 16);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int ky = j - r;
+        if (ky >= 0 && ky < K && !(ED2_SKIP & 2)) {
+          float wr[K];
+#pragma unroll
+          for (int kx = 0; kx < K; ++kx) wr[kx] = wd[ky * K + kx];
+#pragma unroll
+          for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(wr[kx], v[c + kx], acc[r][c]);
+        }
+      }
+    }
+    float psum = 0.f;
+    bf16* drow = dbase + (int64_t)hc * plane_o;
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      bf16x4 o;
+      float y[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        y[c] = hswish(acc[r][c] + bd);
+        o[c] = (bf16)y[c];
+      }
+      if (interior) {
+        psum += (y[0] + y[1]) + (y[2] + y[3]);
+        if (!(ED2_SKIP & 1)) *reinterpret_cast<bf16x4*>(drow + r * a.wo) = o;
+      } else if (oy0 + r0 + r < a.ho) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (ox0 + c0 + c < a.wo) {
+            psum += y[c];
+            drow[r * a.wo + c] = o[c];
+          }
+      }
+    }
+#pragma unroll
+    for (int o = TPC / 2; o > 0; o >>= 1) psum += __shfl_xor(psum, o, 64);
+    if ((tid % TPC) == 0) pool_s[hc] = psum;  // each channel once per tile: one coalesced atomic pass at the end
+  };
+
+  // ---- prologue: parameters of chunks 0 and 1 in slots, chunk 2's in flight, chunk 0's image ----
+  ED2_FETCH(0);
+  ED2_ROTATE();
+  ED2_STASH(0);
+  if (nch > 1) { ED2_FETCH(1); ED2_ROTATE(); ED2_STASH(1); }
+  if (nch > 2) ED2_FETCH(2);
+  ED2_LOAD_IN(0);
+  ED2_ROTATE_IN();
+  ED2_STORE_IN(0);
+  if (nch > 1) ED2_LOAD_IN(1);
+  lds_barrier();  // xs, slots 0/1, (ratio-1) hs[0]
+  expand(0, 0);
+  lds_barrier();
+  for (int c = 0; c < nch; ++c) {
+    ED2_ROTATE();                       // chunk c+2's parameters (issued one iteration ago)
+    ED2_ROTATE_IN();                    // ratio-1: chunk c+1's input tile
+    if (c + 3 < nch) ED2_FETCH(c + 3);
+    if (!EXPAND && c + 2 < nch) ED2_LOAD_IN(c + 2);
+    if (c + 1 < nch) expand(c + 1, (c + 1) & 1);
+    if constexpr (ED2_PHASE_FENCE) __builtin_amdgcn_sched_barrier(0);  // keeps the phases' live ranges apart
+    depthwise(c, c & 1);
+    if (c + 2 < nch) ED2_STASH(c + 2);
+    if (c + 1 < nch) ED2_STORE_IN((c + 1) & 1);
+    lds_barrier();
+  }
+  if (!(ED2_SKIP & 8))
+    for (int c = tid; c < a.hid; c += NT) atomicAdd(a.pool + (int64_t)n * a.hid + c, pool_s[c]);
+#undef ED2_FETCH
+#undef ED2_STASH
+#undef ED2_ROTATE
+#undef ED2_LOAD_IN
+#undef ED2_STORE_IN
+#undef ED2_ROTATE_IN
+}
+
+// ------------------------------------------------------------------------------------------------
 // SE MLP + gate folding into the pw-linear weights
 // ------------------------------------------------------------------------------------------------
 template <typename T>
@@ -730,8 +1081,49 @@ int launch_ed(EdArgs a, hipStream_t st) {
   return AST_E_UNSUPPORTED;
 }
 
+int g_ed_big = 1;  // AST_MB_ED_BIG=0 disables the 16-wave tile (A/B measurements)
+
+template <int K, int UP, bool EXPAND, int TH, int TW, int R, int NT = 512>
+int launch_ed2(EdArgs a, hipStream_t st) {
+  a.tiles_x = (a.wo + TW - 1) / TW;
+  a.tiles_y = (a.ho + TH - 1) / TH;
+  const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.n;
+  if (blocks > 0x7fffffffLL) return AST_E_SHAPE;
+  const size_t lds = ed2_lds_bytes<K, TH, TW, R, NT>(a.cin_pad, EXPAND, a.hid);
+  auto kern = expand_dw2_kernel<K, UP, EXPAND, TH, TW, R, NT>;
+  const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NT), lds, st, a);
+  return (int)hipGetLastError();
+}
+
+// bf16, stride 1: the v2 kernel (two workgroups per CU when the tile's LDS fits 80 KB)
+template <int K, int UP, bool EXPAND>
+int launch_ed2_auto(EdArgs a, hipStream_t st) {
+  if (EXPAND && a.cin_pad > 256) return AST_E_UNSUPPORTED;
+  const int h = a.hid;
+  if (ed2_lds_bytes<K, 8, 32, 2>(a.cin_pad, EXPAND, h) <= kLdsBudget) return launch_ed2<K, UP, EXPAND, 8, 32, 2>(a, st);
+  if (g_ed_big && ed2_lds_bytes<K, 8, 32, 1, 1024>(a.cin_pad, EXPAND, h) <= kLdsBudgetMax)  // 16 waves, 1 WG/CU
+    return launch_ed2<K, UP, EXPAND, 8, 32, 1, 1024>(a, st);
+  if (ed2_lds_bytes<K, 4, 32, 1>(a.cin_pad, EXPAND, h) <= kLdsBudget) return launch_ed2<K, UP, EXPAND, 4, 32, 1>(a, st);
+  if (ed2_lds_bytes<K, 4, 32, 1>(a.cin_pad, EXPAND, h) <= kLdsBudgetMax) return launch_ed2<K, UP, EXPAND, 4, 32, 1>(a, st);
+  return AST_E_UNSUPPORTED;
+}
+
+int g_ed_version = 2;  // AST_MB_ED=1 selects the v1 kernel (A/B measurements)
+
 template <typename T>
 int dispatch_ed(EdArgs a, int k, int s, int up, bool expand, hipStream_t st) {
+  if (sizeof(T) == 2 && s == 1 && g_ed_version >= 2) {
+    int r = AST_E_UNSUPPORTED;
+    if (expand && up == 1 && k == 3) r = launch_ed2_auto<3, 1, true>(a, st);
+    // k5 with narrow inputs: v2 only has the 4-row tile here (the 8-row one exceeds 80 KB of LDS),
+    // whose halo recompute makes it slower than v1 (measured, scripts/bench_mb_blocks.py)
+    else if (expand && up == 1 && k == 5 && (a.cin_pad > 48 || g_ed_version == 3)) r = launch_ed2_auto<5, 1, true>(a, st);
+    else if (!expand && k == 3 && up == 1) r = launch_ed2_auto<3, 1, false>(a, st);
+    else if (!expand && k == 3 && up == 2) r = launch_ed2_auto<3, 2, false>(a, st);
+    if (r != AST_E_UNSUPPORTED) return r;
+  }
   if (expand && up == 1) {
     if (k == 3 && s == 1) return launch_ed<T, 3, 1, 1, true>(a, st);
     if (k == 3 && s == 2) return launch_ed<T, 3, 2, 1, true>(a, st);
@@ -799,6 +1191,16 @@ int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, i
     return AST_E_SHAPE;
   }
   hipStream_t st = (hipStream_t)stream;
+  static const int ver = [] {
+    const char* v = getenv("AST_MB_ED");
+    return v ? atoi(v) : 2;
+  }();
+  g_ed_version = ver;
+  static const int big = [] {
+    const char* v = getenv("AST_MB_ED_BIG");
+    return v ? atoi(v) : 1;
+  }();
+  g_ed_big = big;
   hipError_t e = hipMemsetAsync(pool, 0, sizeof(float) * (size_t)n * hid, st);
   if (e != hipSuccess) return (int)e;
   EdArgs a{x1, x2, c1, n, cin, h, w, h * up, w * up, ho, wo, w1p, b1, hid, expand ? cin_pad : 0, wdw, bdw, d, pool, 0, 0};

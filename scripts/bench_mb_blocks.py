@@ -19,6 +19,8 @@ CASES = [
     ("dec10 40->24 t6 k5 1024", 40, 24, 1, 6, 5, False, 1024, 1),
     ("dec11 24->24 t6 k3 1024", 24, 24, 1, 6, 3, False, 1024, 1),
     ("dec7up 40->40 r1 k3 512->1024", 40, 40, 1, 1, 3, False, 512, 2),
+    ("enc8 80->80 t4 k3 128", 80, 80, 1, 4, 3, True, 128, 1),
+    ("enc11 96->96 t3 k5 128", 96, 96, 1, 3, 5, True, 128, 1),
 ]
 
 

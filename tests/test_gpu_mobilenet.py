@@ -77,7 +77,7 @@ def test_block_fp32(case, hip_device):
     assert rel_inf(y, ref) <= BLOCK_TOL
 
 
-@pytest.mark.parametrize("case", BLOCKS[:3] + BLOCKS[6:9])
+@pytest.mark.parametrize("case", BLOCKS)
 def test_block_bf16(case, hip_device):
     y, ref = run_block(case, hip_device, torch.bfloat16, 950 + case[0] + case[1])
     assert y.dtype == torch.bfloat16
