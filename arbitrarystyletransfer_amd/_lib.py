@@ -61,6 +61,8 @@ SIGNATURES = {
     "ast_mb_pw": (_i, [_i, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _i, _i, _p, _i, _p, _p]),
     "ast_mb_conv3x3_dense": (_i, [_i, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
     "ast_adain_bf16": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _d, _i, _p]),
+    "ast_adaattn_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i, _i, _i, _i]),
+    "ast_adaattn_fwd": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, ctypes.c_size_t, _i, _i, _i, _i, _i, _i, _p]),
 }
 
 ERRORS = {-1: "null pointer", -2: "bad shape", -3: "unsupported configuration"}

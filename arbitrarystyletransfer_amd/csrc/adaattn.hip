@@ -1,0 +1,420 @@
+// AdaAttN (models.py:70-115) for gfx950: attention-weighted style statistics.
+//
+//   q = W_q(IN(c)), k = W_k(IN(s)), v = W_v(s)                       (1x1 convs, no bias)
+//   A = softmax_keys(q^T k)                                           [Nq x Nk] per image
+//   mean = A v,  std = sqrt(relu(A v^2 - mean^2)),  out = std * IN(c) + mean
+// with IN = InstanceNorm2d (biased variance, eps 1e-5, no affine).
+//
+// Three launches per call:
+//   in_stats_kernel    per-(n,c) mean / rstd of content and style (two-pass, one WG per plane)
+//   project_kernel     Q, K, V as [n][Cp][Npad] (Cp = C rounded to 32, Npad = N rounded to 32;
+//                      padding is written as zeros) -- an MFMA-fp32 channel GEMM with the
+//                      instance norm applied while the input is read
+//   attend_f32_kernel  flash-style fused Q K^T -> online softmax -> P [V, V^2] -> epilogue. The
+//                      Nq x Nk score matrix never leaves registers. 4 waves x 32 queries per
+//                      workgroup; K/V blocks of 32 keys are double-buffered in LDS.
+//
+// MFMA orientation (v_mfma_f32_32x32x2_f32, exact fp32): the scores are computed transposed,
+// S^T = K Q^T, so the accumulator has the QUERY on the lane and 16 keys in registers. That tile is
+// directly the B operand of O^T = [V, V^2]^T P^T (summing over keys = S^T's row index), so P
+// never moves between lanes, and O^T again has the query on the lane: the epilogue's stores are
+// 128-byte rows of the NCHW output. The softmax row max / sum need one lane^32 exchange.
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <math.h>
+#include <stdint.h>
+#include "../../include/ast_hip.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kStatThreads = 256;
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ float ld(const float* p) { return *p; }
+__device__ __forceinline__ float ld(const __hip_bfloat16* p) { return __bfloat162float(*p); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < kStatThreads / 64; ++i) t += sh[i];
+  return t;
+}
+
+// InstanceNorm2d statistics: mean and 1/sqrt(biased var + eps) per (n, c) plane; blockIdx.y picks
+// the tensor (0 = content, 1 = style).
+template <typename T>
+__global__ __launch_bounds__(kStatThreads) void in_stats_kernel(const T* __restrict__ c, const T* __restrict__ s,
+                                                                float* __restrict__ stats, int planes, int64_t hwc,
+                                                                int64_t hws, float eps) {
+  __shared__ float sh[kStatThreads / 64];
+  const int p = blockIdx.x;
+  const bool style = blockIdx.y == 1;
+  const int64_t hw = style ? hws : hwc;
+  const T* __restrict__ x = (style ? s : c) + (int64_t)p * hw;
+  float acc = 0.f;
+  for (int64_t i = threadIdx.x; i < hw; i += kStatThreads) acc += ld(x + i);
+  const float mean = block_sum(acc, sh) / (float)hw;
+  acc = 0.f;
+  for (int64_t i = threadIdx.x; i < hw; i += kStatThreads) {
+    const float d = ld(x + i) - mean;
+    acc += d * d;
+  }
+  const float var = block_sum(acc, sh) / (float)hw;
+  if (threadIdx.x == 0) {
+    float* o = stats + (style ? 2 : 0) * (int64_t)planes;
+    o[p] = mean;
+    o[planes + p] = 1.0f / sqrtf(var + eps);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Projections: Y[b][o][p] = sum_c W[o][c] * xn[b][c][p], xn = (x - mean) * rstd (Q, K) or x (V).
+// Workgroup = 4 waves x 32 pixels; each wave holds all Cp output channels (Cp/32 accumulators).
+// W is staged transposed in LDS as Wt[c][o] (row pitch Cp + 32 floats: the two half-waves read
+// rows c and c+1, which then fall in disjoint bank halves).
+// ------------------------------------------------------------------------------------------------
+struct ProjArgs {
+  const void* c;
+  const void* s;
+  const float* wq;
+  const float* wk;
+  const float* wv;
+  const float* stats;  // [4][n*C]: content mean, content rstd, style mean, style rstd
+  float* q;            // [n][Cp][Nqp]
+  float* k;            // [n][Cp][Nkp]
+  float* v;            // [n][Cp][Nkp]
+  int n, C, Cp, nq, nk, nqp, nkp;
+};
+
+template <typename T, int CT>  // CT = Cp / 32 output-channel tiles
+__global__ __launch_bounds__(256) void project_kernel(ProjArgs a) {
+  extern __shared__ float wt[];  // [C_even][Cp + 32]
+  const int which = blockIdx.z;  // 0 = q, 1 = k, 2 = v
+  const int b = blockIdx.y;
+  const int N = which == 0 ? a.nq : a.nk;
+  const int Np = which == 0 ? a.nqp : a.nkp;
+  const int p0 = blockIdx.x * 128;
+  if (p0 >= Np) return;  // whole workgroup: no barrier is skipped by part of it
+  const int C = a.C, Cp = a.Cp, ce = (C + 1) & ~1, pitch = Cp + 32;
+  const float* __restrict__ w = which == 0 ? a.wq : (which == 1 ? a.wk : a.wv);
+  for (int i = threadIdx.x; i < ce * Cp; i += 256) {
+    const int c = i / Cp, o = i - c * Cp;
+    wt[c * pitch + o] = (c < C && o < C) ? w[(int64_t)o * C + c] : 0.f;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int px = p0 + wv * 32 + r;
+  const T* __restrict__ x = (const T*)(which == 0 ? a.c : a.s) + (int64_t)b * C * N;
+  const float* mean = which == 0 ? a.stats : a.stats + 2 * (int64_t)a.n * C;
+  const float* rstd = mean + (int64_t)a.n * C;
+  mean += (int64_t)b * C;
+  rstd += (int64_t)b * C;
+  const bool norm = which != 2, pin = px < N;
+
+  f32x16 acc[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) acc[t] = (f32x16){0.f};
+
+  for (int m = 0; m < ce / 2; ++m) {
+    const int c = 2 * m + h;
+    float xv = 0.f;
+    if (pin && c < C) {
+      xv = ld(x + (int64_t)c * N + px);
+      if (norm) xv = (xv - mean[c]) * rstd[c];
+    }
+    const float* wr = wt + c * pitch + r;
+#pragma unroll
+    for (int t = 0; t < CT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[t * 32], xv, acc[t], 0, 0, 0);
+  }
+  float* __restrict__ y = (which == 0 ? a.q : (which == 1 ? a.k : a.v)) + (int64_t)b * Cp * Np;
+  const int pw = p0 + wv * 32 + r;
+  if (pw < Np) {
+#pragma unroll
+    for (int t = 0; t < CT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int o = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        y[(int64_t)o * Np + pw] = acc[t][i];
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused attention, fp32.
+// ------------------------------------------------------------------------------------------------
+struct AttnArgs {
+  const float* q;  // [n][Cp][Nqp]
+  const float* k;  // [n][Cp][Nkp]
+  const float* v;  // [n][Cp][Nkp]
+  const void* c;   // content [n][C][Nq] (for IN(c) in the epilogue)
+  const float* stats;
+  void* out;  // [n][C][Nq]
+  int n, C, Cp, nq, nk, nqp, nkp, qtiles;
+};
+
+constexpr int BK = 32;        // keys per block
+constexpr int KP = BK;        // K block row pitch (floats): rows c, c+1 -> disjoint bank halves
+constexpr int VP = BK + 4;    // V block row pitch: 16 lanes x f32x4 over 16 distinct bank quads
+
+__device__ __forceinline__ void map_tile(int id, int total, int tiles_per_image, int& b, int& tile) {
+  // XCD-aware order: the hardware places workgroup id on XCD (id % 8). Give each XCD a contiguous
+  // range of (image, tile) so the workgroups of one image share K/V through one L2.
+  int lin = id;
+  if ((total & 7) == 0) lin = (id & 7) * (total >> 3) + (id >> 3);
+  b = lin / tiles_per_image;
+  tile = lin - b * tiles_per_image;
+}
+
+// K/V staging registers as named members. Native ext_vector f32x4, not HIP's float4 struct: its
+// copies lower to memcpy through a private-memory temporary (scratch) that SROA does not remove.
+template <int CT>
+struct KVRegs {
+  f32x4 k0, k1, k2, k3, v0, v1, v2, v3;
+  __device__ __forceinline__ void load(const float* __restrict__ kb, const float* __restrict__ vb, int tid, int nkp,
+                                       int kbase) {
+    const int off = (tid >> 3) * nkp + (tid & 7) * 4 + kbase, step = 32 * nkp;  // +256 threads = +32 rows
+    k0 = *reinterpret_cast<const f32x4*>(kb + off);
+    v0 = *reinterpret_cast<const f32x4*>(vb + off);
+    if constexpr (CT > 1) {
+      k1 = *reinterpret_cast<const f32x4*>(kb + off + step);
+      v1 = *reinterpret_cast<const f32x4*>(vb + off + step);
+    }
+    if constexpr (CT > 2) {
+      k2 = *reinterpret_cast<const f32x4*>(kb + off + 2 * step);
+      v2 = *reinterpret_cast<const f32x4*>(vb + off + 2 * step);
+    }
+    if constexpr (CT > 3) {
+      k3 = *reinterpret_cast<const f32x4*>(kb + off + 3 * step);
+      v3 = *reinterpret_cast<const f32x4*>(vb + off + 3 * step);
+    }
+  }
+  template <int KPITCH, int VPITCH>
+  __device__ __forceinline__ void store(float* ks, float* vs, int tid) const {
+    const int row = tid >> 3, col = (tid & 7) * 4;
+    float* kp = ks + row * KPITCH + col;
+    float* vp = vs + row * VPITCH + col;
+    *reinterpret_cast<f32x4*>(kp) = k0;
+    *reinterpret_cast<f32x4*>(vp) = v0;
+    if constexpr (CT > 1) {
+      *reinterpret_cast<f32x4*>(kp + 32 * KPITCH) = k1;
+      *reinterpret_cast<f32x4*>(vp + 32 * VPITCH) = v1;
+    }
+    if constexpr (CT > 2) {
+      *reinterpret_cast<f32x4*>(kp + 64 * KPITCH) = k2;
+      *reinterpret_cast<f32x4*>(vp + 64 * VPITCH) = v2;
+    }
+    if constexpr (CT > 3) {
+      *reinterpret_cast<f32x4*>(kp + 96 * KPITCH) = k3;
+      *reinterpret_cast<f32x4*>(vp + 96 * VPITCH) = v3;
+    }
+  }
+};
+
+// Lazy rescaling: the running row max is only raised when a block's max exceeds it by more than
+// 2^kRescaleLog2 (log2 units), so exp2 arguments stay <= kRescaleLog2 (no fp32 overflow) and the
+// accumulators are rescaled a handful of times per row instead of whenever the max moves. The
+// final division by the row sum (accumulated against the same stale max) makes this exact.
+constexpr float kRescaleLog2 = 8.0f;
+
+template <typename TO, int CT>
+__global__ __launch_bounds__(256, 1) void attend_f32_kernel(AttnArgs a) {
+  constexpr int CP = CT * 32;
+  // Q tile [CP][128 queries], column XOR-swizzled by (c & 1) << 5 so a wave's two half-waves
+  // (rows c, c+1) read disjoint bank halves; K/V blocks double-buffered.
+  __shared__ float qs[CP * 128];
+  __shared__ float ks[2][CP * KP];
+  __shared__ float vs[2][CP * VP];
+  int b, tile;
+  map_tile(blockIdx.x, gridDim.x, a.qtiles, b, tile);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int q0 = tile * 128;
+  const int qi = q0 + wv * 32 + r;  // this lane's query (column of every accumulator tile)
+
+  {
+    const float* __restrict__ qb = a.q + (int64_t)b * CP * a.nqp + q0;  // nqp is a multiple of 128
+#pragma unroll
+    for (int i = 0; i < CP / 8; ++i) {
+      const int e = tid + i * 256, row = e >> 5, col = (e & 31) * 4;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(qb + (int64_t)row * a.nqp + col);
+      *reinterpret_cast<f32x4*>(&qs[row * 128 + (col ^ ((row & 1) << 5))]) = v;
+    }
+  }
+
+  const float* __restrict__ kb = a.k + (int64_t)b * CP * a.nkp;
+  const float* __restrict__ vb = a.v + (int64_t)b * CP * a.nkp;
+  // K/V block staging: CT f32x4 of K and CT of V per thread and block (row = channel, 8 f32x4
+  // per 32-key row), prefetched into registers one block ahead.
+  KVRegs<CT> kv;
+  f32x16 om[CT], osq[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    om[t] = (f32x16){0.f};
+    osq[t] = (f32x16){0.f};
+  }
+  float mrow = -INFINITY, lsum = 0.f;  // mrow in log2 units
+
+  const int nblk = a.nkp / BK;
+  kv.load(kb, vb, tid, a.nkp, 0);
+  kv.template store<KP, VP>(ks[0], vs[0], tid);
+  const float* qq = &qs[h * 128 + ((wv * 32 + r) ^ (h << 5))];
+  for (int j = 0; j < nblk; ++j) {
+    const int buf = j & 1;
+    if (j + 1 < nblk) kv.load(kb, vb, tid, a.nkp, (j + 1) * BK);
+    __syncthreads();
+
+    // S^T[key][query] for 32 keys (rows) x this wave's 32 queries (lanes); two independent
+    // accumulation chains (alternate channel pairs).
+    f32x16 s0 = (f32x16){0.f}, s1 = (f32x16){0.f};
+    const float* kk = &ks[buf][h * KP + r];
+#pragma unroll
+    for (int m = 0; m < CP / 2; m += 2) {
+      s0 = __builtin_amdgcn_mfma_f32_32x32x2f32(kk[2 * m * KP], qq[2 * m * 128], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_32x32x2f32(kk[(2 * m + 2) * KP], qq[(2 * m + 2) * 128], s1, 0, 0, 0);
+    }
+    f32x16 s = (s0 + s1) * kLog2e;
+
+    // Online softmax over keys (registers + the lane^32 partner).
+    const int kbase = j * BK;
+    {
+      const int lim = a.nk - kbase - 4 * h;  // keys >= nk are masked (only in the last block)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2) < lim) ? s[i] : -INFINITY;
+    }
+    float mb = s[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mb = fmaxf(mb, s[i]);
+    mb = fmaxf(mb, __shfl_xor(mb, 32, 64));
+    if (__builtin_expect(__ballot(mb > mrow + kRescaleLog2) != 0, 0)) {
+      const float mnew = fmaxf(mrow, mb);
+      const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);  // 0 on the first block
+      lsum *= alpha;
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        om[t] *= alpha;
+        osq[t] *= alpha;
+        __builtin_amdgcn_sched_barrier(0);  // one tile at a time: bounded register pressure
+      }
+      mrow = mnew;
+    }
+    float p[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      p[i] = __builtin_amdgcn_exp2f(s[i] - mrow);
+      lsum += p[i];
+    }
+
+    // O^T[ch][query] += V^T P^T and (V^2)^T P^T. MFMA (g, e) pairs k = h with key 4h + 8g + e,
+    // which is exactly register 4g + e of this lane's P; V is read as f32x4 over e. The channel
+    // tiles are innermost: 2*CT independent accumulation chains.
+    const float* vv = &vs[buf][r * VP + 4 * h];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v4[CT];
+#pragma unroll
+      for (int t = 0; t < CT; ++t) v4[t] = *reinterpret_cast<const f32x4*>(vv + t * 32 * VP + 8 * g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int t = 0; t < CT; ++t) {
+          const float ve = e == 0 ? v4[t].x : e == 1 ? v4[t].y : e == 2 ? v4[t].z : v4[t].w;
+          om[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(ve, p[4 * g + e], om[t], 0, 0, 0);
+          osq[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(ve * ve, p[4 * g + e], osq[t], 0, 0, 0);
+        }
+      }
+    }
+    if (j + 1 < nblk) kv.template store<KP, VP>(ks[buf ^ 1], vs[buf ^ 1], tid);
+  }
+
+  // Epilogue: out[b][ch][qi] = std * (c - mean_c) * rstd_c + mean.
+  if (qi >= a.nq) return;
+  const float inv = 1.0f / (lsum + __shfl_xor(lsum, 32, 64));
+  const float* cmean = a.stats + (int64_t)b * a.C;
+  const float* crstd = a.stats + (int64_t)a.n * a.C + (int64_t)b * a.C;
+  const TO* __restrict__ cb = (const TO*)a.c + (int64_t)b * a.C * a.nq;
+  TO* __restrict__ ob = (TO*)a.out + (int64_t)b * a.C * a.nq;
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ch = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (ch < a.C) {
+        const float mean = om[t][i] * inv;
+        float var = fmaf(-mean, mean, osq[t][i] * inv);
+        var = var < 0.f ? 0.f : var;  // ReLU (NaN passes, as torch.relu)
+        const int64_t o = (int64_t)ch * a.nq + qi;
+        const float xn = (ld(cb + o) - cmean[ch]) * crstd[ch];
+        const float y = fmaf(sqrtf(var), xn, mean);
+        if constexpr (sizeof(TO) == 4) ob[o] = y;
+        else ob[o] = __float2bfloat16(y);
+      }
+    }
+}
+
+inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+extern "C" {
+
+size_t ast_adaattn_workspace_bytes(int dtype, int n, int c, int hc, int wc, int hs, int ws) {
+  if (n <= 0 || c <= 0 || hc <= 0 || wc <= 0 || hs <= 0 || ws <= 0) return 0;
+  (void)dtype;
+  const size_t cp = (size_t)round_up(c, 32), nqp = (size_t)round_up(hc * wc, 128), nkp = (size_t)round_up(hs * ws, BK);
+  const size_t stats = 4 * (size_t)n * c;
+  return sizeof(float) * (round_up((int)stats, 64) + (size_t)n * cp * (nqp + 2 * nkp));
+}
+
+int ast_adaattn_fwd(int dtype, const void* content, const void* style, const float* wq, const float* wk,
+                    const float* wv, void* out, void* workspace, size_t workspace_bytes, int n, int c, int hc,
+                    int wc, int hs, int ws, void* stream) {
+  if (!content || !style || !wq || !wk || !wv || !out || !workspace) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hc <= 0 || wc <= 0 || hs <= 0 || ws <= 0) return AST_E_SHAPE;
+  if (dtype != 0) return AST_E_UNSUPPORTED;  // bf16 (1): not yet
+  if (c > 128) return AST_E_UNSUPPORTED;
+  if ((int64_t)hc * wc > (1 << 30) || (int64_t)hs * ws > (1 << 30) || (int64_t)n * c > (1 << 30)) return AST_E_SHAPE;
+  if (workspace_bytes < ast_adaattn_workspace_bytes(dtype, n, c, hc, wc, hs, ws)) return AST_E_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  const int nq = hc * wc, nk = hs * ws, cp = round_up(c, 32), nqp = round_up(nq, 128), nkp = round_up(nk, BK);
+  float* stats = (float*)workspace;
+  float* q = stats + round_up(4 * n * c, 64);
+  float* k = q + (size_t)n * cp * nqp;
+  float* v = k + (size_t)n * cp * nkp;
+
+  hipLaunchKernelGGL(in_stats_kernel<float>, dim3(n * c, 2), dim3(kStatThreads), 0, st, (const float*)content,
+                     (const float*)style, stats, n * c, (int64_t)nq, (int64_t)nk, 1e-5f);
+  ProjArgs pa{content, style, wq, wk, wv, stats, q, k, v, n, c, cp, nq, nk, nqp, nkp};
+  const dim3 pgrid((unsigned)(round_up(nqp > nkp ? nqp : nkp, 128) / 128), (unsigned)n, 3);
+  const size_t plds = sizeof(float) * (size_t)((c + 1) & ~1) * (cp + 32);
+  const int ct = cp / 32;
+  void (*proj)(ProjArgs) = ct == 1 ? project_kernel<float, 1> : ct == 2 ? project_kernel<float, 2>
+                         : ct == 3 ? project_kernel<float, 3> : project_kernel<float, 4>;
+  hipError_t e = hipFuncSetAttribute((const void*)proj, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(proj, pgrid, dim3(256), plds, st, pa);
+  const int qtiles = nqp / 128;
+  AttnArgs aa{q, k, v, content, stats, out, n, c, cp, nq, nk, nqp, nkp, qtiles};
+  const dim3 agrid((unsigned)(n * qtiles));
+  switch (ct) {
+    case 1: hipLaunchKernelGGL((attend_f32_kernel<float, 1>), agrid, dim3(256), 0, st, aa); break;
+    case 2: hipLaunchKernelGGL((attend_f32_kernel<float, 2>), agrid, dim3(256), 0, st, aa); break;
+    case 3: hipLaunchKernelGGL((attend_f32_kernel<float, 3>), agrid, dim3(256), 0, st, aa); break;
+    default: hipLaunchKernelGGL((attend_f32_kernel<float, 4>), agrid, dim3(256), 0, st, aa); break;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -56,6 +56,37 @@ def mean_variance_norm(feat):
     return Fn.mean_variance_norm(feat)
 
 
+class AdaAttN(nn.Module):
+    """AdaAttN, models.py:70-115: attention-weighted style mean/std (SURVEY.md §8f "next" #1).
+
+    Same module tree as the reference (W_q/W_k/W_v 1x1 convs without bias, att_act, std_act and
+    the three parameter-free InstanceNorm2d), so state dicts load unchanged. forward runs
+    ops.adaattn: the Nq x Nk attention matrix is never materialised (one fused HIP kernel).
+    Inference only (it raises under autograd recording rather than silently detaching).
+    """
+
+    def __init__(self, inp_size):
+        super().__init__()
+        self.W_q = nn.Conv2d(inp_size, inp_size, 1, 1, 0, bias=False)
+        self.W_k = nn.Conv2d(inp_size, inp_size, 1, 1, 0, bias=False)
+        self.W_v = nn.Conv2d(inp_size, inp_size, 1, 1, 0, bias=False)
+        self.att_act = nn.Softmax(dim=-1)
+        self.std_act = nn.ReLU(True)
+        self.inst_norm_1 = nn.InstanceNorm2d(inp_size)
+        self.inst_norm_2 = nn.InstanceNorm2d(inp_size)
+        self.inst_norm = nn.InstanceNorm2d(inp_size)
+        self.inp_size = inp_size
+
+    def forward(self, content_map, style_map):
+        if torch.is_grad_enabled() and (content_map.requires_grad or style_map.requires_grad
+                                        or any(p.requires_grad for p in self.parameters())):
+            raise NotImplementedError("AdaAttN on the HIP path is inference-only: run it under torch.no_grad() "
+                                      "or with frozen parameters and inputs")
+        if content_map.shape[1] != self.inp_size:
+            raise ops.HipOpError(f"expected {self.inp_size} channels, got {content_map.shape[1]}")
+        return ops.adaattn(content_map, style_map, self.W_q.weight, self.W_k.weight, self.W_v.weight)
+
+
 def _needs_grad(x, module):
     return torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in module.parameters()))
 

@@ -250,3 +250,41 @@ def mean_variance_norm(x: torch.Tensor):
     """models.py:64-68 (unbiased var + 1e-5)."""
     mean, std = channel_stats(x, unbiased=True, eps=1e-5)
     return plane_normalize(x, mean, std)
+
+
+# ------------------------------------------------------------------------------------------------
+# AdaAttN (models.py:70-115)
+# ------------------------------------------------------------------------------------------------
+
+ADAATTN_MAX_CHANNELS = 128
+
+
+def adaattn(content: torch.Tensor, style: torch.Tensor, wq: torch.Tensor, wk: torch.Tensor, wv: torch.Tensor):
+    """AdaAttN.forward (models.py:81-115) as three launches: instance-norm statistics, the Q/K/V
+    1x1 projections, and one fused attention kernel (scores, online softmax, attention-weighted
+    mean and std, `std * IN(content) + mean`). content [N, C, H, W], style [N, C, Hs, Ws] fp32;
+    wq/wk/wv are the [C, C, 1, 1] (or [C, C]) Conv2d weights."""
+    content = _dev(content, "content_map")
+    style = _dev(style, "style_map")
+    if content.dim() != 4 or style.dim() != 4 or content.shape[:2] != style.shape[:2]:
+        raise HipOpError(f"AdaAttN needs NCHW maps with equal (N, C): {tuple(content.shape)} vs {tuple(style.shape)}")
+    n, c, hc, wc = (int(s) for s in content.shape)
+    hs, ws = int(style.shape[2]), int(style.shape[3])
+    if hc * wc == 1 or hs * ws == 1:   # InstanceNorm2d's own error (models.py:78-80)
+        raise ValueError("Expected more than 1 spatial element when training (InstanceNorm2d in AdaAttN)")
+    if c > ADAATTN_MAX_CHANNELS:
+        raise HipOpError(f"AdaAttN HIP kernel supports C <= {ADAATTN_MAX_CHANNELS}, got {c}")
+    w = []
+    for name, t in (("W_q", wq), ("W_k", wk), ("W_v", wv)):
+        t = _dev(t.detach().float(), name)
+        if t.numel() != c * c:
+            raise HipOpError(f"{name} must be [{c}, {c}, 1, 1], got {tuple(t.shape)}")
+        w.append(t)
+    out = torch.empty_like(content)
+    nbytes = lib().ast_adaattn_workspace_bytes(0, n, c, hc, wc, hs, ws)
+    ws_buf = torch.empty((nbytes,), dtype=torch.uint8, device=content.device)
+    flops = 6 * n * c * (hc * wc) * (hs * ws)   # S (2C) + P[V, V^2] (4C) per score
+    check(_timed(f"adaattn {c}ch {hc}x{wc}<-{hs}x{ws}", flops, content.device, lambda: lib().ast_adaattn_fwd(
+        0, ptr(content), ptr(style), ptr(w[0]), ptr(w[1]), ptr(w[2]), ptr(out), ptr(ws_buf), nbytes,
+        n, c, hc, wc, hs, ws, stream_ptr(content.device))), "adaattn")
+    return out

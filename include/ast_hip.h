@@ -285,6 +285,20 @@ int ast_mb_conv3x3_dense(int dtype_in, int dtype_out, const void* x, const float
 int ast_adain_bf16(const void* content, const void* style, void* out, int n, int c, int hc, int wc,
                    int hs, int ws, double alpha, int swap_style_stats, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * AdaAttN (models.py:70-115; SURVEY §8f "next" #1): attention-weighted style statistics.
+ *   q = W_q(IN(content)), k = W_k(IN(style)), v = W_v(style)     (1x1 convs, no bias)
+ *   A = softmax over style pixels of q^T k; mean = A v; std = sqrt(relu(A v^2 - mean^2))
+ *   out = std * IN(content) + mean,   IN = InstanceNorm2d (biased var, eps 1e-5, no affine)
+ * content [n][c][hc][wc], style [n][c][hs][ws], out like content (dtype 0 = fp32);
+ * wq/wk/wv [c][c] fp32 (the Conv2d weights [c][c][1][1]). c <= 128.
+ * workspace: device scratch of ast_adaattn_workspace_bytes() bytes (Q, K, V, statistics). */
+size_t ast_adaattn_workspace_bytes(int dtype, int n, int c, int hc, int wc, int hs, int ws);
+int ast_adaattn_fwd(int dtype, const void* content, const void* style, const float* wq,
+                    const float* wk, const float* wv, void* out, void* workspace,
+                    size_t workspace_bytes, int n, int c, int hc, int wc, int hs, int ws,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

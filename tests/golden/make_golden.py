@@ -191,6 +191,7 @@ def main():
                         img=img.detach().numpy(), tv=tv.detach().numpy(), tv_grad=img.grad.numpy())
     train_step_golden(R, enc_wb, dec_wb)
     mobilenet_golden(R)
+    adaattn_golden(R)
     print("golden vectors written to", HERE)
 
 
@@ -254,6 +255,30 @@ def mobilenet_golden(R):
         np.savez_compressed(os.path.join(HERE, name + ".npz"), seeds=np.array(seeds), shape=np.array(shape), **r)
 
 
+def adaattn_golden(R):
+    """AdaAttN (models.py:70-115) from the reference's own class, live-init weights. Two regimes:
+    'diffuse' scales W_q and W_k by 1/8 (softmax spread over many style pixels: the std term is
+    well conditioned) and 'live' keeps the live init (logits of tens: near-argmax attention, where
+    E[v^2] - mean^2 cancels). Ragged spatial sizes, content and style of different sizes."""
+    out = {}
+    cases = (("c16", 16, (2, 16, 6, 10), (2, 16, 7, 5), 931),
+             ("c128", 128, (1, 128, 16, 12), (1, 128, 9, 20), 935),
+             ("c40", 40, (2, 40, 8, 8), (2, 40, 8, 8), 939))
+    with torch.no_grad():
+        for tag, c, cshape, sshape, seed in cases:
+            m = synth.live_init_(R["AdaAttN"](c), seed).eval()
+            x = torch.from_numpy((synth.uniform(seed + 1, int(np.prod(cshape))) * 1.5 + 0.25).astype(np.float32).reshape(cshape))
+            y = torch.from_numpy((synth.uniform(seed + 2, int(np.prod(sshape))) * 2.0 - 0.5).astype(np.float32).reshape(sshape))
+            out[f"{tag}_content"], out[f"{tag}_style"] = x.numpy(), y.numpy()
+            out[f"{tag}_wq"], out[f"{tag}_wk"] = m.W_q.weight.numpy().copy(), m.W_k.weight.numpy().copy()
+            out[f"{tag}_wv"] = m.W_v.weight.numpy().copy()
+            out[f"{tag}_live"] = m(x, y).numpy()
+            m.W_q.weight.mul_(0.125)
+            m.W_k.weight.mul_(0.125)
+            out[f"{tag}_diffuse"] = m(x, y).numpy()
+    np.savez_compressed(os.path.join(HERE, "adaattn.npz"), **out)
+
+
 def train_step_golden(R, enc_wb, dec_wb):
     """One AdaIN training step assembled from the reference's own functions
     exactly as train.py:191-300 assembles its losses: lifted PretrainedEncoder / AdaIN /
@@ -314,5 +339,7 @@ if __name__ == "__main__":
     if "--mobilenet" in sys.argv:
         torch.manual_seed(0)
         mobilenet_golden(load_reference())
+    elif "--adaattn" in sys.argv:
+        adaattn_golden(load_reference())
     else:
         main()

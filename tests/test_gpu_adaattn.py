@@ -1,0 +1,101 @@
+"""GPU parity for AdaAttN (models.py:70-115; SURVEY.md §8f "next" #1): the fused HIP attention
+path against the reference's own AdaAttN outputs (tests/golden/adaattn.npz) and against the CPU
+oracle (oracle/ref_cpu.adaattn) on seeded inputs of ragged shapes.
+
+Tolerances (fp32, written here): rel_inf = max|a-b|/max|b|.
+  * diffuse attention (the well-conditioned regime): 1e-4;
+  * live-init weights (near-argmax attention, logits of tens): 1e-3 -- std = sqrt(E[v^2] - mean^2)
+    cancels there, so summation-order rounding of the two fp32 bmm's is amplified (the north-star
+    fp32 bar).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from arbitrarystyletransfer_amd import models, ops, synth
+from oracle import ref_cpu as R
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "adaattn.npz")
+TOL = {"diffuse": 1e-4, "live": 1e-3}
+
+
+def rel_inf(a, b):
+    a = np.asarray(a.detach().cpu() if torch.is_tensor(a) else a, np.float64)
+    b = np.asarray(b.detach().cpu() if torch.is_tensor(b) else b, np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def T(a, dev="cuda"):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+@pytest.mark.parametrize("tag", ["c16", "c128", "c40"])
+@pytest.mark.parametrize("regime", ["diffuse", "live"])
+def test_adaattn_vs_reference_golden(tag, regime):
+    g = np.load(GOLDEN)
+    sc = 0.125 if regime == "diffuse" else 1.0
+    out = ops.adaattn(T(g[f"{tag}_content"]), T(g[f"{tag}_style"]), T(g[f"{tag}_wq"] * sc),
+                      T(g[f"{tag}_wk"] * sc), T(g[f"{tag}_wv"]))
+    torch.cuda.synchronize()
+    err = rel_inf(out, g[f"{tag}_{regime}"])
+    assert err <= TOL[regime], (tag, regime, err)
+
+
+def _case(seed, n, c, hc, wc, hs, ws, qk_scale):
+    x = synth.uniform(seed, n * c * hc * wc).astype(np.float32).reshape(n, c, hc, wc) * 2.0 - 0.3
+    y = synth.uniform(seed + 1, n * c * hs * ws).astype(np.float32).reshape(n, c, hs, ws) * 1.5
+    w = [synth.conv_weight(seed + 2 + i, c, c, 1).reshape(c, c) for i in range(3)]
+    w[0] = w[0] * qk_scale
+    w[1] = w[1] * qk_scale
+    return x, y, w
+
+
+@pytest.mark.parametrize("shape", [
+    (1, 32, 8, 16, 8, 16),     # one query tile, one key block
+    (2, 64, 13, 11, 5, 7),     # ragged queries and keys (Nk = 35: a 3-key last block)
+    (3, 96, 2, 1, 1, 2),       # two pixels each (tiny planes)
+    (1, 128, 40, 40, 33, 31),  # Nq = 1600 (13 query tiles), Nk = 1023
+    (2, 8, 17, 3, 2, 40),      # C = 8 (one padded channel tile), tall/wide maps
+    (1, 100, 12, 12, 16, 16),  # C not a multiple of 32 or 8
+])
+def test_adaattn_vs_oracle(shape):
+    n, c, hc, wc, hs, ws = shape
+    x, y, w = _case(1000 + c, n, c, hc, wc, hs, ws, 0.15)
+    out = ops.adaattn(T(x), T(y), *(T(t) for t in w))
+    ref = R.adaattn(torch.from_numpy(x), torch.from_numpy(y), *(torch.from_numpy(t) for t in w))
+    torch.cuda.synchronize()
+    assert rel_inf(out, ref) <= 1e-4, (shape, rel_inf(out, ref))
+
+
+def test_adaattn_large_logits_stable():
+    """Logits in the hundreds: the online softmax must not overflow (torch's softmax subtracts
+    the row max too)."""
+    x, y, w = _case(77, 1, 64, 16, 16, 16, 16, 6.0)
+    out = ops.adaattn(T(x), T(y), *(T(t) for t in w))
+    ref = R.adaattn(torch.from_numpy(x), torch.from_numpy(y), *(torch.from_numpy(t) for t in w))
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert rel_inf(out, ref) <= 1e-3
+
+
+def test_adaattn_module_and_guards():
+    c = 32
+    m = synth.live_init_(models.AdaAttN(c), 5).cuda().eval()
+    x = torch.rand(2, c, 9, 7, device="cuda")
+    y = torch.rand(2, c, 6, 6, device="cuda")
+    with torch.no_grad():
+        out = m(x, y)
+    ref = R.adaattn(x.cpu(), y.cpu(), m.W_q.weight.cpu(), m.W_k.weight.cpu(), m.W_v.weight.cpu())
+    assert rel_inf(out, ref) <= 1e-3
+    with pytest.raises(NotImplementedError):
+        m(x, y)  # parameters require grad and autograd is recording
+    with pytest.raises(ops.HipOpError):
+        ops.adaattn(torch.rand(1, 129, 4, 4, device="cuda"), torch.rand(1, 129, 4, 4, device="cuda"),
+                    *(torch.rand(129, 129, device="cuda") for _ in range(3)))
+    with pytest.raises(ops.HipOpError):
+        ops.adaattn(x, torch.rand(2, c + 1, 6, 6, device="cuda"), m.W_q.weight, m.W_k.weight, m.W_v.weight)
