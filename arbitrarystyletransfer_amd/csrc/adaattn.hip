@@ -20,7 +20,6 @@
 // never moves between lanes, and O^T again has the query on the lane: the epilogue's stores are
 // 128-byte rows of the NCHW output. The softmax row max / sum need one lane^32 exchange.
 #include <hip/hip_runtime.h>
-#include <hip/hip_bf16.h>
 #include <math.h>
 #include <stdint.h>
 #include "../../include/ast_hip.h"
@@ -34,7 +33,11 @@ constexpr int kStatThreads = 256;
 constexpr float kLog2e = 1.4426950408889634f;
 
 __device__ __forceinline__ float ld(const float* p) { return *p; }
-__device__ __forceinline__ float ld(const __hip_bfloat16* p) { return __bfloat162float(*p); }
+__device__ __forceinline__ float ld(const __bf16* p) { return (float)*p; }
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -358,8 +361,277 @@ __global__ __launch_bounds__(256, 1) void attend_f32_kernel(AttnArgs a) {
         const int64_t o = (int64_t)ch * a.nq + qi;
         const float xn = (ld(cb + o) - cmean[ch]) * crstd[ch];
         const float y = fmaf(sqrtf(var), xn, mean);
-        if constexpr (sizeof(TO) == 4) ob[o] = y;
-        else ob[o] = __float2bfloat16(y);
+        ob[o] = (TO)y;
+      }
+    }
+}
+
+
+// ================================================================================================
+// bf16 path (bf16 storage, fp32 accumulation): the MobileNet-variant AST runs in bf16.
+//   Q, K  [n][Np][Cp]  pixel-major (an MFMA-bf16 A/B fragment is 8 consecutive channels)
+//   V, V2 [n][Cp][Nkp] channel-major; V is centred by the style's channel mean before the 1x1 conv
+//         (V' = W_v (s - mean_s); the epilogue adds W_v mean_s back, which the softmax weights
+//         summing to 1 makes exact) and V2 = bf16(V'^2) is squared from the fp32 projection, so
+//         E[v^2] - mean^2 is formed from small, accurately rounded terms.
+// ================================================================================================
+struct ProjB16Args {
+  const bf16* c;
+  const bf16* s;
+  const float* wq;
+  const float* wk;
+  const float* wv;
+  const float* stats;  // [4][n*C]
+  bf16* q;             // [n][Nqp][Cp]
+  bf16* k;             // [n][Nkp][Cp]
+  bf16* v;             // [n][Cp][Nkp]
+  bf16* v2;            // [n][Cp][Nkp]
+  int n, C, Cp, nq, nk, nqp, nkp;
+};
+
+template <int CT>
+__global__ __launch_bounds__(256) void project_bf16_kernel(ProjB16Args a) {
+  extern __shared__ float wt[];  // [C_even][Cp + 32]
+  const int which = blockIdx.z;  // 0 = q, 1 = k, 2 = v (+ v2)
+  const int b = blockIdx.y;
+  const int N = which == 0 ? a.nq : a.nk;
+  const int Np = which == 0 ? a.nqp : a.nkp;
+  const int p0 = blockIdx.x * 128;
+  if (p0 >= Np) return;
+  const int C = a.C, Cp = a.Cp, ce = (C + 1) & ~1, pitch = Cp + 32;
+  const float* __restrict__ w = which == 0 ? a.wq : (which == 1 ? a.wk : a.wv);
+  for (int i = threadIdx.x; i < ce * Cp; i += 256) {
+    const int c = i / Cp, o = i - c * Cp;
+    wt[c * pitch + o] = (c < C && o < C) ? w[(int64_t)o * C + c] : 0.f;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int px = p0 + wv * 32 + r;
+  const bf16* __restrict__ x = (which == 0 ? a.c : a.s) + (int64_t)b * C * N;
+  const float* mean = which == 0 ? a.stats : a.stats + 2 * (int64_t)a.n * C;
+  const float* rstd = mean + (int64_t)a.n * C;
+  mean += (int64_t)b * C;
+  rstd += (int64_t)b * C;
+  const bool pin = px < N, pm = which == 0 ? false : true;
+  (void)pm;
+
+  f32x16 acc[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) acc[t] = (f32x16){0.f};
+  for (int m = 0; m < ce / 2; ++m) {
+    const int c = 2 * m + h;
+    float xv = 0.f;
+    if (pin && c < C) {
+      xv = (float)x[(int64_t)c * N + px] - mean[c];
+      if (which != 2) xv *= rstd[c];
+    }
+    const float* wr = wt + c * pitch + r;
+    if (which == 2) {  // D[o][pixel]: lane = pixel
+#pragma unroll
+      for (int t = 0; t < CT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[t * 32], xv, acc[t], 0, 0, 0);
+    } else {           // D[pixel][o]: lane = output channel
+#pragma unroll
+      for (int t = 0; t < CT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(xv, wr[t * 32], acc[t], 0, 0, 0);
+    }
+  }
+  const int pw0 = p0 + wv * 32;
+  if (which == 2) {
+    bf16* __restrict__ y = a.v + (int64_t)b * Cp * Np;
+    bf16* __restrict__ y2 = a.v2 + (int64_t)b * Cp * Np;
+    const int pw = pw0 + r;
+    if (pw < Np) {
+#pragma unroll
+      for (int t = 0; t < CT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int o = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          const float vv = acc[t][i];
+          y[(int64_t)o * Np + pw] = (bf16)vv;
+          y2[(int64_t)o * Np + pw] = (bf16)(vv * vv);
+        }
+    }
+  } else {
+    bf16* __restrict__ y = (which == 0 ? a.q : a.k) + (int64_t)b * Np * Cp;
+#pragma unroll
+    for (int t = 0; t < CT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int p = pw0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (p < Np) y[(int64_t)p * Cp + t * 32 + r] = (bf16)acc[t][i];
+      }
+  }
+}
+
+// mean of V over the style pixels, per (n, o): W_v mean_s (added back in the epilogue).
+__global__ __launch_bounds__(128) void vmean_kernel(const float* __restrict__ wv, const float* __restrict__ stats,
+                                                    float* __restrict__ vmean, int n, int C) {
+  const int b = blockIdx.x;
+  const float* ms = stats + 2 * (int64_t)n * C + (int64_t)b * C;
+  for (int o = threadIdx.x; o < C; o += 128) {
+    float acc = 0.f;
+    for (int c = 0; c < C; ++c) acc = fmaf(wv[(int64_t)o * C + c], ms[c], acc);
+    vmean[(int64_t)b * C + o] = acc;
+  }
+}
+
+struct AttnB16Args {
+  const bf16* q;   // [n][Nqp][Cp]
+  const bf16* k;   // [n][Nkp][Cp]
+  const bf16* v;   // [n][Cp][Nkp]
+  const bf16* v2;  // [n][Cp][Nkp]
+  const bf16* c;   // content [n][C][Nq]
+  const float* stats;
+  const float* vmean;  // [n][C]
+  bf16* out;
+  int n, C, Cp, nq, nk, nqp, nkp, qtiles;
+};
+
+// 8 waves x 32 queries per workgroup, 32-key blocks, v_mfma_f32_32x32x16_bf16.
+//   S^T = K Q^T: A = K from LDS ([key][Cp + 8] bf16 rows: 16-byte reads, conflict-free), B = this
+//   lane's Q fragment (registers, loaded once).
+//   P = bf16(exp2(S - m)) straight from the accumulator: registers 8s..8s+7 are the B fragment of
+//   k-step s with key order 16s + 8(j>>2) + 4h + (j&3); the A operand (V^T) is read in that same
+//   key order as two 8-byte reads from [ch][36] rows (72-byte pitch: conflict-free).
+constexpr int KPB = 8;   // K row padding (bf16)
+constexpr int VPB = 36;  // V row pitch (bf16)
+
+template <int CT>
+__global__ __launch_bounds__(512, 1) void attend_bf16_kernel(AttnB16Args a) {
+  constexpr int CP = CT * 32, KROW = CP + KPB;
+  __shared__ __attribute__((aligned(16))) bf16 ks[2][BK * KROW];
+  __shared__ __attribute__((aligned(16))) bf16 vs[2][CP * VPB];
+  __shared__ __attribute__((aligned(16))) bf16 v2s[2][CP * VPB];
+  int b, tile;
+  map_tile(blockIdx.x, gridDim.x, a.qtiles, b, tile);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int qi = tile * 256 + wv * 32 + r;
+
+  bf16x8 qf[CP / 16];
+  {
+    const bf16* qp = a.q + ((int64_t)b * a.nqp + qi) * CP + 8 * h;
+#pragma unroll
+    for (int s = 0; s < CP / 16; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
+  }
+
+  // staging: K block = 32 rows x CP bf16 (CP/8 16-byte pieces per row); V, V2 blocks = CP rows x
+  // 32 keys (4 pieces per row). One piece of each per thread (CP = 128), fewer threads otherwise.
+  const bf16* __restrict__ kb = a.k + (int64_t)b * a.nkp * CP;
+  const bf16* __restrict__ vb = a.v + (int64_t)b * CP * a.nkp;
+  const bf16* __restrict__ v2b = a.v2 + (int64_t)b * CP * a.nkp;
+  constexpr int NPIECE = CP * 4;  // = 32 * CP / 8
+  const bool stager = tid < NPIECE;
+  const int krow = tid / (CP / 8), kcol = (tid % (CP / 8)) * 8;
+  const int vrow = tid >> 2, vcol = (tid & 3) * 8;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  u32x4 kr = {0, 0, 0, 0}, vr = kr, v2r = kr;
+  auto gload = [&](int kbase) {
+    if (stager) {
+      kr = *reinterpret_cast<const u32x4*>(kb + (int64_t)(kbase + krow) * CP + kcol);
+      vr = *reinterpret_cast<const u32x4*>(vb + (int64_t)vrow * a.nkp + kbase + vcol);
+      v2r = *reinterpret_cast<const u32x4*>(v2b + (int64_t)vrow * a.nkp + kbase + vcol);
+    }
+  };
+  auto lstore = [&](int buf) {
+    if (stager) {
+      *reinterpret_cast<u32x4*>(&ks[buf][krow * KROW + kcol]) = kr;
+      u32x2* pv = reinterpret_cast<u32x2*>(&vs[buf][vrow * VPB + vcol]);
+      pv[0] = (u32x2){vr[0], vr[1]};
+      pv[1] = (u32x2){vr[2], vr[3]};
+      u32x2* pv2 = reinterpret_cast<u32x2*>(&v2s[buf][vrow * VPB + vcol]);
+      pv2[0] = (u32x2){v2r[0], v2r[1]};
+      pv2[1] = (u32x2){v2r[2], v2r[3]};
+    }
+  };
+
+  f32x16 om[CT], osq[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    om[t] = (f32x16){0.f};
+    osq[t] = (f32x16){0.f};
+  }
+  float mrow = -INFINITY, lsum = 0.f;
+  const int nblk = a.nkp / BK;
+  gload(0);
+  lstore(0);
+  for (int j = 0; j < nblk; ++j) {
+    const int buf = j & 1;
+    if (j + 1 < nblk) gload((j + 1) * BK);
+    __syncthreads();
+
+    f32x16 s = (f32x16){0.f};
+    const bf16* kk = &ks[buf][r * KROW + 8 * h];
+#pragma unroll
+    for (int st = 0; st < CP / 16; ++st)
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(kk + 16 * st), qf[st], s, 0, 0, 0);
+    s *= kLog2e;
+    {
+      const int lim = a.nk - j * BK - 4 * h;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2) < lim) ? s[i] : -INFINITY;
+    }
+    float mb = s[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mb = fmaxf(mb, s[i]);
+    mb = fmaxf(mb, __shfl_xor(mb, 32, 64));
+    if (__builtin_expect(__ballot(mb > mrow + kRescaleLog2) != 0, 0)) {
+      const float mnew = fmaxf(mrow, mb);
+      const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
+      lsum *= alpha;
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        om[t] *= alpha;
+        osq[t] *= alpha;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mrow = mnew;
+    }
+    bf16x8 pb[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const bf16 pv = (bf16)__builtin_amdgcn_exp2f(s[i] - mrow);
+      lsum += (float)pv;  // normalise by the weights actually applied
+      pb[i >> 3][i & 7] = pv;
+    }
+
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        const int off = (t * 32 + r) * VPB + 16 * st + 4 * h;
+        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(&vs[buf][off]);
+        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(&vs[buf][off + 8]);
+        const bf16x4 lo2 = *reinterpret_cast<const bf16x4*>(&v2s[buf][off]);
+        const bf16x4 hi2 = *reinterpret_cast<const bf16x4*>(&v2s[buf][off + 8]);
+        const bf16x8 va = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        const bf16x8 va2 = __builtin_shufflevector(lo2, hi2, 0, 1, 2, 3, 4, 5, 6, 7);
+        om[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb[st], om[t], 0, 0, 0);
+        osq[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va2, pb[st], osq[t], 0, 0, 0);
+      }
+    }
+    if (j + 1 < nblk) lstore(buf ^ 1);
+  }
+
+  if (qi >= a.nq) return;
+  const float inv = 1.0f / (lsum + __shfl_xor(lsum, 32, 64));
+  const float* cmean = a.stats + (int64_t)b * a.C;
+  const float* crstd = a.stats + (int64_t)a.n * a.C + (int64_t)b * a.C;
+  const float* vm = a.vmean + (int64_t)b * a.C;
+  const bf16* __restrict__ cb = a.c + (int64_t)b * a.C * a.nq;
+  bf16* __restrict__ ob = a.out + (int64_t)b * a.C * a.nq;
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ch = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (ch < a.C) {
+        const float mean = om[t][i] * inv;  // of the centred V
+        float var = fmaf(-mean, mean, osq[t][i] * inv);
+        var = var < 0.f ? 0.f : var;
+        const int64_t o = (int64_t)ch * a.nq + qi;
+        const float xn = ((float)cb[o] - cmean[ch]) * crstd[ch];
+        ob[o] = (bf16)fmaf(sqrtf(var), xn, mean + vm[ch]);
       }
     }
 }
@@ -368,14 +640,43 @@ inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
 }  // namespace
 
+
+namespace {
+
+struct AttnLayout {  // workspace carve-up (bytes), shared by the size query and the launcher
+  int cp, nqp, nkp;
+  size_t stats, vmean, q, k, v, v2, total;
+};
+
+AttnLayout attn_layout(int dtype, int n, int c, int nq, int nk) {
+  AttnLayout L;
+  L.cp = round_up(c, 32);
+  L.nqp = round_up(nq, dtype == 0 ? 128 : 256);
+  L.nkp = round_up(nk, BK);
+  const size_t es = dtype == 0 ? 4 : 2;
+  auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+  L.stats = 0;
+  L.vmean = al(4 * sizeof(float) * (size_t)n * c);
+  L.q = L.vmean + al(sizeof(float) * (size_t)n * c);
+  L.k = L.q + al(es * (size_t)n * L.cp * L.nqp);
+  L.v = L.k + al(es * (size_t)n * L.cp * L.nkp);
+  L.v2 = L.v + al(es * (size_t)n * L.cp * L.nkp);
+  L.total = L.v2 + (dtype == 0 ? 0 : al(es * (size_t)n * L.cp * L.nkp));
+  return L;
+}
+
+template <typename K>
+hipError_t set_lds(K kern, size_t bytes) {
+  return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+}  // namespace
+
 extern "C" {
 
 size_t ast_adaattn_workspace_bytes(int dtype, int n, int c, int hc, int wc, int hs, int ws) {
-  if (n <= 0 || c <= 0 || hc <= 0 || wc <= 0 || hs <= 0 || ws <= 0) return 0;
-  (void)dtype;
-  const size_t cp = (size_t)round_up(c, 32), nqp = (size_t)round_up(hc * wc, 128), nkp = (size_t)round_up(hs * ws, BK);
-  const size_t stats = 4 * (size_t)n * c;
-  return sizeof(float) * (round_up((int)stats, 64) + (size_t)n * cp * (nqp + 2 * nkp));
+  if (n <= 0 || c <= 0 || hc <= 0 || wc <= 0 || hs <= 0 || ws <= 0 || (dtype != 0 && dtype != 1)) return 0;
+  return attn_layout(dtype, n, c, hc * wc, hs * ws).total;
 }
 
 int ast_adaattn_fwd(int dtype, const void* content, const void* style, const float* wq, const float* wk,
@@ -383,37 +684,57 @@ int ast_adaattn_fwd(int dtype, const void* content, const void* style, const flo
                     int wc, int hs, int ws, void* stream) {
   if (!content || !style || !wq || !wk || !wv || !out || !workspace) return AST_E_NULLPTR;
   if (n <= 0 || c <= 0 || hc <= 0 || wc <= 0 || hs <= 0 || ws <= 0) return AST_E_SHAPE;
-  if (dtype != 0) return AST_E_UNSUPPORTED;  // bf16 (1): not yet
+  if (dtype != 0 && dtype != 1) return AST_E_UNSUPPORTED;
   if (c > 128) return AST_E_UNSUPPORTED;
-  if ((int64_t)hc * wc > (1 << 30) || (int64_t)hs * ws > (1 << 30) || (int64_t)n * c > (1 << 30)) return AST_E_SHAPE;
+  if ((int64_t)hc * wc > (1 << 28) || (int64_t)hs * ws > (1 << 28) || (int64_t)n * c > (1 << 28)) return AST_E_SHAPE;
   if (workspace_bytes < ast_adaattn_workspace_bytes(dtype, n, c, hc, wc, hs, ws)) return AST_E_SHAPE;
   hipStream_t st = (hipStream_t)stream;
-  const int nq = hc * wc, nk = hs * ws, cp = round_up(c, 32), nqp = round_up(nq, 128), nkp = round_up(nk, BK);
-  float* stats = (float*)workspace;
-  float* q = stats + round_up(4 * n * c, 64);
-  float* k = q + (size_t)n * cp * nqp;
-  float* v = k + (size_t)n * cp * nkp;
-
-  hipLaunchKernelGGL(in_stats_kernel<float>, dim3(n * c, 2), dim3(kStatThreads), 0, st, (const float*)content,
-                     (const float*)style, stats, n * c, (int64_t)nq, (int64_t)nk, 1e-5f);
-  ProjArgs pa{content, style, wq, wk, wv, stats, q, k, v, n, c, cp, nq, nk, nqp, nkp};
+  const int nq = hc * wc, nk = hs * ws;
+  const AttnLayout L = attn_layout(dtype, n, c, nq, nk);
+  const int cp = L.cp, nqp = L.nqp, nkp = L.nkp, ct = cp / 32;
+  unsigned char* wsb = (unsigned char*)workspace;
+  float* stats = (float*)(wsb + L.stats);
   const dim3 pgrid((unsigned)(round_up(nqp > nkp ? nqp : nkp, 128) / 128), (unsigned)n, 3);
   const size_t plds = sizeof(float) * (size_t)((c + 1) & ~1) * (cp + 32);
-  const int ct = cp / 32;
-  void (*proj)(ProjArgs) = ct == 1 ? project_kernel<float, 1> : ct == 2 ? project_kernel<float, 2>
-                         : ct == 3 ? project_kernel<float, 3> : project_kernel<float, 4>;
-  hipError_t e = hipFuncSetAttribute((const void*)proj, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(proj, pgrid, dim3(256), plds, st, pa);
-  const int qtiles = nqp / 128;
-  AttnArgs aa{q, k, v, content, stats, out, n, c, cp, nq, nk, nqp, nkp, qtiles};
-  const dim3 agrid((unsigned)(n * qtiles));
-  switch (ct) {
-    case 1: hipLaunchKernelGGL((attend_f32_kernel<float, 1>), agrid, dim3(256), 0, st, aa); break;
-    case 2: hipLaunchKernelGGL((attend_f32_kernel<float, 2>), agrid, dim3(256), 0, st, aa); break;
-    case 3: hipLaunchKernelGGL((attend_f32_kernel<float, 3>), agrid, dim3(256), 0, st, aa); break;
-    default: hipLaunchKernelGGL((attend_f32_kernel<float, 4>), agrid, dim3(256), 0, st, aa); break;
+  hipError_t e;
+
+  if (dtype == 0) {
+    float* q = (float*)(wsb + L.q);
+    float* k = (float*)(wsb + L.k);
+    float* v = (float*)(wsb + L.v);
+    hipLaunchKernelGGL(in_stats_kernel<float>, dim3(n * c, 2), dim3(kStatThreads), 0, st, (const float*)content,
+                       (const float*)style, stats, n * c, (int64_t)nq, (int64_t)nk, 1e-5f);
+    ProjArgs pa{content, style, wq, wk, wv, stats, q, k, v, n, c, cp, nq, nk, nqp, nkp};
+    void (*proj)(ProjArgs) = ct == 1 ? project_kernel<float, 1> : ct == 2 ? project_kernel<float, 2>
+                           : ct == 3 ? project_kernel<float, 3> : project_kernel<float, 4>;
+    if ((e = set_lds(proj, plds)) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(proj, pgrid, dim3(256), plds, st, pa);
+    const int qtiles = nqp / 128;
+    AttnArgs aa{q, k, v, content, stats, out, n, c, cp, nq, nk, nqp, nkp, qtiles};
+    void (*att)(AttnArgs) = ct == 1 ? attend_f32_kernel<float, 1> : ct == 2 ? attend_f32_kernel<float, 2>
+                          : ct == 3 ? attend_f32_kernel<float, 3> : attend_f32_kernel<float, 4>;
+    hipLaunchKernelGGL(att, dim3((unsigned)(n * qtiles)), dim3(256), 0, st, aa);
+    return (int)hipGetLastError();
   }
+
+  bf16* q = (bf16*)(wsb + L.q);
+  bf16* k = (bf16*)(wsb + L.k);
+  bf16* v = (bf16*)(wsb + L.v);
+  bf16* v2 = (bf16*)(wsb + L.v2);
+  float* vmean = (float*)(wsb + L.vmean);
+  hipLaunchKernelGGL(in_stats_kernel<bf16>, dim3(n * c, 2), dim3(kStatThreads), 0, st, (const bf16*)content,
+                     (const bf16*)style, stats, n * c, (int64_t)nq, (int64_t)nk, 1e-5f);
+  hipLaunchKernelGGL(vmean_kernel, dim3(n), dim3(128), 0, st, wv, stats, vmean, n, c);
+  ProjB16Args pa{(const bf16*)content, (const bf16*)style, wq, wk, wv, stats, q, k, v, v2, n, c, cp, nq, nk, nqp, nkp};
+  void (*proj)(ProjB16Args) = ct == 1 ? project_bf16_kernel<1> : ct == 2 ? project_bf16_kernel<2>
+                            : ct == 3 ? project_bf16_kernel<3> : project_bf16_kernel<4>;
+  if ((e = set_lds(proj, plds)) != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(proj, pgrid, dim3(256), plds, st, pa);
+  const int qtiles = nqp / 256;
+  AttnB16Args aa{q, k, v, v2, (const bf16*)content, stats, vmean, (bf16*)out, n, c, cp, nq, nk, nqp, nkp, qtiles};
+  void (*att)(AttnB16Args) = ct == 1 ? attend_bf16_kernel<1> : ct == 2 ? attend_bf16_kernel<2>
+                           : ct == 3 ? attend_bf16_kernel<3> : attend_bf16_kernel<4>;
+  hipLaunchKernelGGL(att, dim3((unsigned)(n * qtiles)), dim3(512), 0, st, aa);
   return (int)hipGetLastError();
 }
 

@@ -260,12 +260,18 @@ ADAATTN_MAX_CHANNELS = 128
 
 
 def adaattn(content: torch.Tensor, style: torch.Tensor, wq: torch.Tensor, wk: torch.Tensor, wv: torch.Tensor):
-    """AdaAttN.forward (models.py:81-115) as three launches: instance-norm statistics, the Q/K/V
-    1x1 projections, and one fused attention kernel (scores, online softmax, attention-weighted
-    mean and std, `std * IN(content) + mean`). content [N, C, H, W], style [N, C, Hs, Ws] fp32;
-    wq/wk/wv are the [C, C, 1, 1] (or [C, C]) Conv2d weights."""
-    content = _dev(content, "content_map")
-    style = _dev(style, "style_map")
+    """AdaAttN.forward (models.py:81-115) as HIP launches: instance-norm statistics, the Q/K/V 1x1
+    projections, and one fused attention kernel (scores, online softmax, attention-weighted mean
+    and std, `std * IN(content) + mean`); the Nq x Nk attention matrix is never materialised.
+    content [N, C, H, W], style [N, C, Hs, Ws], both fp32 or both bf16 (bf16 storage, fp32
+    accumulation); wq/wk/wv are the [C, C, 1, 1] (or [C, C]) Conv2d weights (any float dtype)."""
+    if not isinstance(content, torch.Tensor) or not isinstance(style, torch.Tensor):
+        raise TypeError("content_map and style_map must be tensors")
+    if content.dtype == torch.bfloat16:
+        dtype_code, content = 1, _dev_typed(content, "content_map", torch.bfloat16)
+        style = _dev_typed(style, "style_map", torch.bfloat16)
+    else:
+        dtype_code, content, style = 0, _dev(content, "content_map"), _dev(style, "style_map")
     if content.dim() != 4 or style.dim() != 4 or content.shape[:2] != style.shape[:2]:
         raise HipOpError(f"AdaAttN needs NCHW maps with equal (N, C): {tuple(content.shape)} vs {tuple(style.shape)}")
     n, c, hc, wc = (int(s) for s in content.shape)
@@ -276,15 +282,18 @@ def adaattn(content: torch.Tensor, style: torch.Tensor, wq: torch.Tensor, wk: to
         raise HipOpError(f"AdaAttN HIP kernel supports C <= {ADAATTN_MAX_CHANNELS}, got {c}")
     w = []
     for name, t in (("W_q", wq), ("W_k", wk), ("W_v", wv)):
-        t = _dev(t.detach().float(), name)
+        if t.device.type != "cuda":
+            raise HipOpError(f"{name} is on {t.device}; arbitrarystyletransfer_amd runs on MI355X (HIP) devices only")
+        t = t.detach().to(torch.float32).contiguous()
         if t.numel() != c * c:
             raise HipOpError(f"{name} must be [{c}, {c}, 1, 1], got {tuple(t.shape)}")
         w.append(t)
     out = torch.empty_like(content)
-    nbytes = lib().ast_adaattn_workspace_bytes(0, n, c, hc, wc, hs, ws)
+    nbytes = lib().ast_adaattn_workspace_bytes(dtype_code, n, c, hc, wc, hs, ws)
     ws_buf = torch.empty((nbytes,), dtype=torch.uint8, device=content.device)
     flops = 6 * n * c * (hc * wc) * (hs * ws)   # S (2C) + P[V, V^2] (4C) per score
-    check(_timed(f"adaattn {c}ch {hc}x{wc}<-{hs}x{ws}", flops, content.device, lambda: lib().ast_adaattn_fwd(
-        0, ptr(content), ptr(style), ptr(w[0]), ptr(w[1]), ptr(w[2]), ptr(out), ptr(ws_buf), nbytes,
+    tag = f"adaattn{' bf16' if dtype_code else ''} {c}ch {hc}x{wc}<-{hs}x{ws}"
+    check(_timed(tag, flops, content.device, lambda: lib().ast_adaattn_fwd(
+        dtype_code, ptr(content), ptr(style), ptr(w[0]), ptr(w[1]), ptr(w[2]), ptr(out), ptr(ws_buf), nbytes,
         n, c, hc, wc, hs, ws, stream_ptr(content.device))), "adaattn")
     return out

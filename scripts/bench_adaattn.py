@@ -37,3 +37,4 @@ if __name__ == "__main__":
         run(8, 128, 64, 64, dt)
         run(4, 128, 128, 128, dt)
         run(32, 128, 128, 128, dt, iters=2)
+        run(32, 128, 128, 128, dt, iters=2)
