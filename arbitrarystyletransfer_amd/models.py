@@ -470,39 +470,57 @@ class AutoEncoder(nn.Module):
 
 
 class AST(nn.Module):
-    """The reference AST (models.py:393-582) with AdaIN as the stylisation op.
+    """The reference AST (models.py:393-582), MobileNet-variant encoder -> per-layer stylisation
+    at enc_out_layers -> ada_out -> decoder.
 
-    The reference class does not run (SyntaxError at models.py:459, missing
-    ada_att_2/ada_out); its AdaAttN op is off the hot path. This keeps the constructor and forward
-    signatures and return values (models.py:395,425,529-533) and the encode structure
-    (models.py:535-566) with AdaIN(content_i, style_i) at enc_out_layers. Inference only: BN uses
-    running statistics, so the reference's eval()/train() toggling in encode() is not needed.
+    The reference class does not run (SyntaxError at models.py:459; ada_att_2 and
+    ada_out are used by encode (models.py:557-565) but not defined). This keeps the constructor
+    and forward signatures and return values (models.py:395,425,529-533) and the encode structure
+    (models.py:535-566). `attention=False` (default, the north-star path) stylises each layer with
+    AdaIN(content_i, style_i); `attention=True` uses the reference's own choice, AdaAttN modules
+    `ada_att_1` / `ada_att_2` (models.py:407-408, 557-558), each over enc_out_channels.
+    Inference only: BN uses running statistics, so the reference's eval()/train() toggling in
+    encode() is not needed.
     """
 
-    def __init__(self, style_layers=[4, 7, 10, 12, 16], content_layers=[4, 7, 10, 12, 16], exporting=False):
+    def __init__(self, style_layers=[4, 7, 10, 12, 16], content_layers=[4, 7, 10, 12, 16], exporting=False,
+                 attention=False):
         super().__init__()
         self._style_layers = style_layers
         self._content_layers = content_layers
         self._exporting = exporting
         self._enc = Encoder(self._exporting)
         self._dec = Decoder(self._exporting)
-        self._adain = AdaIN()
+        self._attention = attention
+        if attention:
+            self.ada_att_1 = AdaAttN(enc_out_channels)
+            self.ada_att_2 = AdaAttN(enc_out_channels)
+        else:
+            self._adain = AdaIN()
         self.ada_out = DepthWiseConv(enc_out_channels * 2, enc_out_channels, 1, EXPAND_RATIO, use_norm=False,
                                      use_identity=False)
 
-    def load_live_init(self, enc_seed: int = 5, dec_seed: int = 6, ada_seed: int = 7):
+    def load_live_init(self, enc_seed: int = 5, dec_seed: int = 6, ada_seed: int = 7, att_seed: int = 8):
         synth.live_init_(self._enc, enc_seed)
         synth.live_init_(self._dec, dec_seed)
         synth.live_init_(self.ada_out, ada_seed)
+        if self._attention:
+            synth.live_init_(self.ada_att_1, att_seed)
+            synth.live_init_(self.ada_att_2, att_seed + 1)
         return self
+
+    def stylize_maps(self, content_maps, style_maps):
+        """Per-layer stylisation of the enc_out_layers maps (models.py:557-558)."""
+        if self._attention:
+            return self.ada_att_1(content_maps[0], style_maps[0]), self.ada_att_2(content_maps[1], style_maps[1])
+        for m in content_maps:     # AdaIN reads content + style and writes its output
+            _trace_io(3 * m.numel() * m.element_size())
+        return self._adain(content_maps[0], style_maps[0]), self._adain(content_maps[1], style_maps[1])
 
     def encode(self, content_img, style_img, detach=False, return_maps=False):
         content_maps = self._enc(content_img, out_layers=enc_out_layers)
         style_maps = self._enc(style_img, out_layers=enc_out_layers)
-        for m in content_maps:     # AdaIN reads content + style and writes its output
-            _trace_io(3 * m.numel() * m.element_size())
-        st1 = self._adain(content_maps[0], style_maps[0])
-        st2 = self._adain(content_maps[1], style_maps[1])
+        st1, st2 = self.stylize_maps(content_maps, style_maps)
         stylized_map = self.ada_out(st1, st2)
         self._last_content_maps = content_maps
         if return_maps:

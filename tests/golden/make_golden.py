@@ -276,6 +276,26 @@ def adaattn_golden(R):
             m.W_q.weight.mul_(0.125)
             m.W_k.weight.mul_(0.125)
             out[f"{tag}_diffuse"] = m(x, y).numpy()
+
+        # the reference AST's attention path (models.py:535-566): Encoder -> AdaAttN(layer 12),
+        # AdaAttN(layer 14) -> cat -> ada_out -> Decoder(exporting), from the reference's modules
+        enc = synth.live_init_(R["Encoder"](), 5).eval()
+        dec = synth.live_init_(R["Decoder"](), 6).eval()
+        ada = synth.live_init_(R["AutoEncoder"]().ada_out, 7).eval()
+        att1 = synth.live_init_(R["AdaAttN"](128), 8).eval()
+        att2 = synth.live_init_(R["AdaAttN"](128), 9).eval()
+        cimg = torch.from_numpy(synth.image(951, (1, 3, 128, 96)))
+        simg = torch.from_numpy(synth.image(952, (1, 3, 112, 128)))
+        cm = enc(cimg, out_layers=[12, 14])
+        sm = enc(simg, out_layers=[12, 14])
+        a12, a14 = att1(cm[0], sm[0]), att2(cm[1], sm[1])
+        t = ada(torch.cat((a12, a14), dim=1))
+        dec.exporting = True
+        y = dec(t)
+        out.update(ast_content=cimg.numpy(), ast_style=simg.numpy(), ast_att12=a12.numpy(), ast_att14=a14.numpy(),
+                   ast_t=t.numpy(), ast_out=y.numpy())
+        for k, v in list(att1.state_dict().items()):
+            out[f"ast_att1_checksum:{k}"] = synth.checksum(v.numpy())
     np.savez_compressed(os.path.join(HERE, "adaattn.npz"), **out)
 
 

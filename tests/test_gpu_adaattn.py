@@ -138,3 +138,42 @@ def test_adaattn_bf16_vs_reference_golden(regime):
     # live regime: near-argmax attention on logits of tens; bf16 Q/K carry 2^-9 relative error,
     # i.e. ~0.1 on such a logit (a 10 % change of its weight), so the bar there is 0.1 (measured 0.068)
     assert rel_inf(out.float(), ref) <= (2e-2 if regime == "diffuse" else 0.1), rel_inf(out.float(), ref)
+
+
+def test_attention_ast_vs_reference_golden():
+    """models.AST(attention=True): the reference AST's AdaAttN path end to end (fp32) against the
+    reference modules' output (tests/golden/adaattn.npz, make_golden.adaattn_golden)."""
+    g = np.load(GOLDEN)
+    ast = models.AST(exporting=True, attention=True).load_live_init().eval().cuda()
+    assert sorted(k for k in ast.state_dict() if k.startswith("ada_att")) == [
+        "ada_att_1.W_k.weight", "ada_att_1.W_q.weight", "ada_att_1.W_v.weight",
+        "ada_att_2.W_k.weight", "ada_att_2.W_q.weight", "ada_att_2.W_v.weight"]
+    c, s = T(g["ast_content"]), T(g["ast_style"])
+    with torch.no_grad():
+        a12, a14, t = ast.encode(c, s, return_maps=True)
+        y = ast(c, s)
+    torch.cuda.synchronize()
+    # live-init AdaAttN is the near-argmax regime (1e-3 bar, measured 6-7e-4); ada_out maps those
+    # deviations onto a small t (max |t| 0.02), measured 1.5e-3 of max|t|; the image: 2.5e-6
+    assert rel_inf(a12, g["ast_att12"]) <= 1e-3 and rel_inf(a14, g["ast_att14"]) <= 1e-3
+    assert rel_inf(t, g["ast_t"]) <= 3e-3
+    assert rel_inf(y, g["ast_out"]) <= 1e-4
+
+
+def test_attention_ast_bf16_runs_and_tracks_fp32():
+    """bf16 attention AST at a 256^2 image: finite, and within bf16 distance of the fp32 module.
+    W_q/W_k scaled by 1/8 (the diffuse regime): with the live init's logits of tens, bf16 Q/K
+    rounding alone re-ranks near-tied keys (see test_adaattn_bf16_vs_reference_golden)."""
+    c = torch.from_numpy(synth.image(961, (2, 3, 256, 256))).cuda()
+    s = torch.from_numpy(synth.image(962, (2, 3, 256, 256))).cuda()
+    ast = models.AST(exporting=True, attention=True).load_live_init().eval().cuda()
+    with torch.no_grad():
+        for m in (ast.ada_att_1, ast.ada_att_2):
+            m.W_q.weight.mul_(0.125)
+            m.W_k.weight.mul_(0.125)
+        t32 = ast.encode(c, s)
+        astb = ast.to(torch.bfloat16)
+        tb = astb.encode(c.bfloat16(), s.bfloat16())
+        y = astb(c.bfloat16(), s.bfloat16())
+    assert torch.isfinite(y.float()).all() and y.shape == (2, 3, 256, 256)
+    assert rel_inf(tb.float(), t32) <= 0.2   # encoder bf16 rounding amplified by IN (as the AdaIN path)

@@ -219,3 +219,18 @@ def test_adaattn_module_tree_matches_reference():
     sd = m.state_dict()
     assert sorted(sd) == ["W_k.weight", "W_q.weight", "W_v.weight"]
     assert all(tuple(v.shape) == (128, 128, 1, 1) for v in sd.values())
+
+
+def test_attention_ast_oracle_matches_reference(golden):
+    """The reference's attention AST path (Encoder -> AdaAttN x2 -> cat -> ada_out ->
+    Decoder(exporting), models.py:535-566) vs oracle.mb_style_transfer(att_sds=...)."""
+    from arbitrarystyletransfer_amd import models
+    g = golden("adaattn")
+    enc, dec, ada = _mb_state_dicts()
+    att = [synth.live_init_(models.AdaAttN(128), seed).state_dict() for seed in (8, 9)]
+    for k, v in att[0].items():
+        np.testing.assert_allclose(synth.checksum(v.numpy()), g[f"ast_att1_checksum:{k}"], rtol=1e-6)
+    c, s = torch.from_numpy(g["ast_content"]), torch.from_numpy(g["ast_style"])
+    with torch.no_grad():
+        y = R.mb_style_transfer(c, s, enc, dec, ada, exporting=True, att_sds=att)
+    assert rel_inf(y, g["ast_out"]) < 1e-5
