@@ -34,6 +34,7 @@ from arbitrarystyletransfer_amd import models, ops, synth  # noqa: E402
 METRIC = "stylised images/sec at 512x512 bs=8, 1->8 MI355X; encoder MFMA %-of-peak"
 PEAK_FP32_MFMA_TF = 157.3       # MI355X_MICROARCH.md: 256 CU x 4 SIMD x 64 FLOP/clk x 2.4 GHz
 PEAK_HBM_GBS = 8000.0
+PEAK_BF16_MFMA_TF = 2516.6      # dense bf16 MFMA (MI355X_MICROARCH.md), no sparsity
 
 
 def parse():
@@ -48,6 +49,9 @@ def parse():
     p.add_argument("--mode", choices=["fwd", "train", "mobilenet"], default="fwd",
                    help="fwd: config 2 (the headline metric); train: config 3/4 AdaIN training step; "
                         "mobilenet: config 5")
+    p.add_argument("--attention", action="store_true",
+                   help="mobilenet mode: stylise with the reference AST's AdaAttN (SURVEY §8f next #1) "
+                        "instead of AdaIN")
     return p.parse_args()
 
 
@@ -117,7 +121,7 @@ def mobilenet_bench(args, dev, rank, world):
     from arbitrarystyletransfer_amd import mobilenetv2
     B, S = args.batch or 32, args.size or 1024
     bf = torch.bfloat16
-    net = models.AST(exporting=True).load_live_init().eval().to(dev).to(bf)
+    net = models.AST(exporting=True, attention=args.attention).load_live_init().eval().to(dev).to(bf)
     content = torch.from_numpy(synth.image(821 + 2 * rank, (B, 3, S, S))).to(dev).to(bf)
     style = torch.from_numpy(synth.image(822 + 2 * rank, (B, 3, S, S))).to(dev).to(bf)
 
@@ -150,7 +154,13 @@ def mobilenet_bench(args, dev, rank, world):
     assert torch.isfinite(out.float()).all(), "non-finite output"
     recs = timer.results()
     fam = {}
+    attn = [0.0, 0.0, 0]
     for tag, nb, ms in recs:
+        if tag.startswith("adaattn"):   # FLOP-tagged (MFMA-bound), not byte-tagged
+            attn[0] += nb
+            attn[1] += ms
+            attn[2] += 1
+            continue
         key = tag.split(" ")[0] + " " + tag.split(" ")[1]
         a = fam.setdefault(key, [0.0, 0.0, 0])
         a[0] += -nb
@@ -158,16 +168,22 @@ def mobilenet_bench(args, dev, rank, world):
         a[2] += 1
     kernels = {k: {"ms_per_step": v[1] / args.steps, "launches_per_step": v[2] // args.steps,
                    "algorithmic_gbs": v[0] / (v[1] * 1e-3) / 1e9} for k, v in fam.items()}
+    if attn[2]:
+        tf = attn[0] / (attn[1] * 1e-3) / 1e12
+        kernels["adaattn bf16"] = {"ms_per_step": attn[1] / args.steps, "launches_per_step": attn[2] // args.steps,
+                                   "tflops": tf, "frac_of_bf16_mfma_peak": tf / PEAK_BF16_MFMA_TF}
     step_s = elapsed / args.steps
     achieved = fused_min_bytes / step_s / 1e9
     ed = fam.get("mb expand_dw")
     result = {
-        "metric": "stylised images/sec, MobileNet variant bs=32 1024x1024 bf16 (config 5)",
+        "metric": "stylised images/sec, MobileNet variant bs=32 1024x1024 bf16 (config 5)"
+                  + (", AdaAttN stylisation" if args.attention else ""),
         "value": B * world * args.steps / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (live-init MobileNet weights, U[0,1) images), resident in HBM",
-        "config": {"workload": f"config 5: MobileNet-style Encoder (content+style) -> AdaIN@[12,14] -> ada_out -> "
+        "config": {"workload": f"config 5: MobileNet-style Encoder (content+style) -> "
+                               f"{'AdaAttN' if args.attention else 'AdaIN'}@[12,14] -> ada_out -> "
                                f"Decoder(exporting), bs={B}/GPU {S}x{S}, bf16 storage / fp32 accumulate",
                    "global_batch": B * world, "image_size": S, "parallelism": f"batch-sharded x{world}"},
         "roofline": {"bound": "hbm", "kernel": "whole step vs the block-fused minimum traffic (SURVEY §8d)",
@@ -179,7 +195,7 @@ def mobilenet_bench(args, dev, rank, world):
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         threads = args.cpu_threads or min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-        result["cpu_baseline"] = cpu_baseline_mobilenet(S, args.cpu_seconds, threads)
+        result["cpu_baseline"] = cpu_baseline_mobilenet(S, args.cpu_seconds, threads, args.attention)
     if rank == 0:
         print(json.dumps(result), flush=True)
 
@@ -198,20 +214,23 @@ def _cpu_model():
     return f"{cpu_model}, {platform.machine()}"
 
 
-def cpu_baseline_mobilenet(size, seconds, threads):
+def cpu_baseline_mobilenet(size, seconds, threads, attention=False):
     """The CPU oracle of the MobileNet variant (fp32: the reference has no bf16 CPU path)."""
     from oracle import ref_cpu as R
     torch.set_num_threads(threads)
     sds = []
     for m, seed in ((models.Encoder(), 5), (models.Decoder(), 6), (models.AutoEncoder().ada_out, 7)):
         sds.append(synth.live_init_(m, seed).eval().state_dict())
+    kw = {}
+    if attention:
+        kw["att_sds"] = [synth.live_init_(models.AdaAttN(128), seed).state_dict() for seed in (8, 9)]
     c = torch.from_numpy(synth.image(821, (1, 3, size, size)))
     s = torch.from_numpy(synth.image(822, (1, 3, size, size)))
     with torch.no_grad():
-        R.mb_style_transfer(c[:, :, :64, :64], s[:, :, :64, :64], *sds)
+        R.mb_style_transfer(c[:, :, :64, :64], s[:, :, :64, :64], *sds, **kw)
         n, t0 = 0, time.perf_counter()
         while True:
-            R.mb_style_transfer(c, s, *sds)
+            R.mb_style_transfer(c, s, *sds, **kw)
             n += 1
             dt = time.perf_counter() - t0
             if dt >= seconds or n >= 64:
