@@ -63,6 +63,11 @@ SIGNATURES = {
     "ast_adain_bf16": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _d, _i, _p]),
     "ast_adaattn_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i, _i, _i, _i]),
     "ast_adaattn_fwd": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, ctypes.c_size_t, _i, _i, _i, _i, _i, _i, _p]),
+    "ast_soft_hist_f32": (_i, [_p, _i, _ll, _f, _p, _p]),
+    "ast_emd_loss_f32": (_i, [_p, _p, _i, _f, _p, _p, _p, _p]),
+    "ast_soft_hist_backward_f32": (_i, [_p, _i, _ll, _f, _p, _p, _i, _p]),
+    "ast_range_loss_f32": (_i, [_p, _ll, _f, _p, _p, _p, _i, _p]),
+    "ast_sqdiff_mean_f32": (_i, [_p, _p, _ll, _f, _p, _p, _p, _i, _p]),
 }
 
 ERRORS = {-1: "null pointer", -2: "bad shape", -3: "unsupported configuration"}

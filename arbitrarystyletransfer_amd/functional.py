@@ -415,3 +415,97 @@ class TVLossFn(torch.autograd.Function):
         check(lib().ast_tv_loss_f32(ptr(img), n * c, h, w, 1.0, ptr(_dev(g, "grad")), None, ptr(dx), 0, _s(img)),
               "tv_loss")
         return dx
+
+
+# ------------------------------------------------------------------------------------------------
+# Histogram / range / pixel losses (train.py:255-269; SURVEY.md §8f "next" #2)
+# ------------------------------------------------------------------------------------------------
+
+HIST_BINS = 256   # HistLayerBase.K, losses.py:44
+
+
+def soft_histogram(x):
+    """SingleDimHistLayer.forward (losses.py:52-57) of x [B, C, H, W] (or [B, C, H]):
+    [B, 256], normalised by C*H as the reference (x.size(1) * x.size(2))."""
+    x = _dev(x, "x")
+    b = x.shape[0]
+    hist = _empty((b, HIST_BINS), x)
+    check(lib().ast_soft_hist_f32(ptr(x), b, x.numel() // b, 1.0 / (x.shape[1] * x.shape[2]), ptr(hist), _s(x)),
+          "soft_hist")
+    return hist
+
+
+class HistLossFn(torch.autograd.Function):
+    """weight * compute_hist_loss(x, y) (losses.py:84-87): EMD between the soft histograms of x
+    and y, mean over the batch; y is data (no gradient), as at train.py:261."""
+
+    @staticmethod
+    def forward(ctx, x, y, weight):
+        x, y = _dev(x, "t_cs"), _dev(y, "style_map")
+        if x.shape[0] != y.shape[0]:
+            raise HipOpError(f"hist loss: batch mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
+        hx, hy = soft_histogram(x), soft_histogram(y)
+        loss = _scalar(x)
+        check(lib().ast_emd_loss_f32(ptr(hx), ptr(hy), x.shape[0], float(weight), None, ptr(loss), None, _s(x)),
+              "emd_loss")
+        ctx.save_for_backward(x, hx, hy)
+        ctx.weight = float(weight)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, hx, hy = ctx.saved_tensors
+        g = _dev(g, "grad")
+        b = x.shape[0]
+        ghist = torch.empty_like(hx)
+        check(lib().ast_emd_loss_f32(ptr(hx), ptr(hy), b, ctx.weight, ptr(g), None, ptr(ghist), _s(x)), "emd_loss")
+        dx = torch.empty_like(x)
+        check(lib().ast_soft_hist_backward_f32(ptr(x), b, x.numel() // b, 1.0 / (x.shape[1] * x.shape[2]),
+                                               ptr(ghist), ptr(dx), 0, _s(x)), "soft_hist_backward")
+        return dx, None, None
+
+
+class RangeLossFn(torch.autograd.Function):
+    """weight * compute_content_loss(x, torch.clip(x.detach(), 0, 1)) (train.py:259)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        x = _dev(x, "x")
+        loss = _scalar(x)
+        check(lib().ast_range_loss_f32(ptr(x), x.numel(), float(weight), None, ptr(loss), None, 0, _s(x)),
+              "range_loss")
+        ctx.save_for_backward(x)
+        ctx.weight = float(weight)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        check(lib().ast_range_loss_f32(ptr(x), x.numel(), ctx.weight, ptr(_dev(g, "grad")), None, ptr(dx), 0, _s(x)),
+              "range_loss")
+        return dx, None
+
+
+class SqDiffMeanFn(torch.autograd.Function):
+    """weight * ((y - x) ** 2).mean() with y constant (train.py:268: content_imgs.detach())."""
+
+    @staticmethod
+    def forward(ctx, x, y, weight):
+        x, y = _dev(x, "x"), _dev(y, "y")
+        if x.shape != y.shape:
+            raise HipOpError(f"sqdiff: shape mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
+        loss = _scalar(x)
+        check(lib().ast_sqdiff_mean_f32(ptr(x), ptr(y), x.numel(), float(weight), None, ptr(loss), None, 0, _s(x)),
+              "sqdiff")
+        ctx.save_for_backward(x, y)
+        ctx.weight = float(weight)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        check(lib().ast_sqdiff_mean_f32(ptr(x), ptr(y), x.numel(), ctx.weight, ptr(_dev(g, "grad")), None, ptr(dx), 0,
+                                        _s(x)), "sqdiff")
+        return dx, None, None

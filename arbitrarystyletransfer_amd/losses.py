@@ -1,15 +1,18 @@
 """Drop-in for the reference losses.py: gram_matrix, compute_content_loss, compute_style_loss,
-tv_loss. Forward and backward are HIP kernels (functional.py).
-
-The soft-histogram / Earth-Mover loss (losses.py:8-87, `compute_hist_loss`) is off the
-north-star path (SURVEY.md §8f "next") and raises here.
-"""
+tv_loss and the soft-histogram / Earth-Mover loss compute_hist_loss
+(losses.py:8-87; §8f "next" #2), with the SingleDimHistLayer / EarthMoversDistanceLoss modules
+and the module-level `hist` / `earth_movers` instances. Forward and backward are HIP kernels
+(functional.py)."""
 from __future__ import annotations
 
 from . import functional as Fn
 
+import torch
+import torch.nn as nn
+
 __all__ = ["gram_matrix", "compute_content_loss", "compute_style_loss", "tv_loss", "compute_hist_loss",
-           "content_mvn_loss", "style_loss_weighted"]
+           "content_mvn_loss", "style_loss_weighted", "EarthMoversDistanceLoss", "HistLayerBase",
+           "SingleDimHistLayer", "hist", "earth_movers", "out_of_range_loss", "pixel_mse_loss"]
 
 
 def gram_matrix(tensor):
@@ -44,6 +47,46 @@ def style_loss_weighted(t_cs_map, style_map, weight: float = 1.0):
     return Fn.StyleLossFn.apply(t_cs_map, style_map.detach(), float(weight))
 
 
-def compute_hist_loss(t_cs, style_map):
-    raise NotImplementedError("compute_hist_loss (losses.py:84-87) is off the AdaIN hot path "
-                              "(SURVEY.md §8f rank 2); not implemented on HIP yet")
+class EarthMoversDistanceLoss(nn.Module):
+    """losses.py:8-22: per-row sum of squared CDF differences of (Batch x Bins) inputs."""
+
+    def forward(self, x, y):
+        from .ops import emd_rows
+        return emd_rows(x, y)
+
+
+class HistLayerBase(nn.Module):
+    """losses.py:40-48: K = 256 bins of width L = 1/K on [0, 1], sigmoid sharpness W = L/2.5."""
+
+    def __init__(self):
+        super().__init__()
+        self.K = Fn.HIST_BINS
+        self.L = 1 / self.K
+        self.W = self.L / 2.5
+
+
+class SingleDimHistLayer(HistLayerBase):
+    """losses.py:51-57: one soft histogram over all values of each image, / (x.size(1)*x.size(2))."""
+
+    def forward(self, x):
+        return Fn.soft_histogram(x)
+
+
+hist = SingleDimHistLayer()                # losses.py:79
+earth_movers = EarthMoversDistanceLoss()   # losses.py:80
+
+
+def compute_hist_loss(t_cs, style_map, weight: float = 1.0):
+    """losses.py:84-87: earth_movers(hist(t_cs), hist(style_map)).mean(), differentiable in t_cs
+    (style_map is data, train.py:261). `weight` fuses the caller's scale (train.py: 1e-5)."""
+    return Fn.HistLossFn.apply(t_cs, style_map.detach(), float(weight))
+
+
+def out_of_range_loss(img, weight: float = 1e8):
+    """train.py:259: compute_content_loss(img, torch.clip(img.detach(), 0.0, 1.0)) * 1e8."""
+    return Fn.RangeLossFn.apply(img, float(weight))
+
+
+def pixel_mse_loss(out, target, weight: float = 100.0):
+    """train.py:268: ((target.detach() - out) ** 2).mean() * 100."""
+    return Fn.SqDiffMeanFn.apply(out, target.detach(), float(weight))

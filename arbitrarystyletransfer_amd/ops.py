@@ -297,3 +297,16 @@ def adaattn(content: torch.Tensor, style: torch.Tensor, wq: torch.Tensor, wk: to
         dtype_code, ptr(content), ptr(style), ptr(w[0]), ptr(w[1]), ptr(w[2]), ptr(out), ptr(ws_buf), nbytes,
         n, c, hc, wc, hs, ws, stream_ptr(content.device))), "adaattn")
     return out
+
+
+def emd_rows(hx: torch.Tensor, hy: torch.Tensor):
+    """EarthMoversDistanceLoss.forward (losses.py:11-22) on [B, 256] histograms: [B] values."""
+    hx, hy = _dev(hx, "x"), _dev(hy, "y")
+    if hx.dim() != 2 or hx.shape != hy.shape or hx.shape[1] != 256:
+        raise HipOpError(f"earth movers: expected two [B, 256] tensors, got {tuple(hx.shape)} / {tuple(hy.shape)}")
+    b = hx.shape[0]
+    out = torch.zeros((b,), device=hx.device, dtype=torch.float32)
+    for i in range(b):   # one scalar per row: the kernel accumulates weight/n * row sums
+        check(lib().ast_emd_loss_f32(ptr(hx[i:i + 1]), ptr(hy[i:i + 1]), 1, 1.0, None, ptr(out[i:i + 1]), None,
+                                     stream_ptr(hx.device)), "emd")
+    return out

@@ -299,6 +299,35 @@ int ast_adaattn_fwd(int dtype, const void* content, const void* style, const flo
                     size_t workspace_bytes, int n, int c, int hc, int wc, int hs, int ws,
                     void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Remaining train.py loss terms (SURVEY §8f "next" #2). Scalars are accumulated (atomicAdd) into
+ * *loss, which the caller zeroes; gscale (device scalar, may be NULL = 1) scales gradients.
+ * ------------------------------------------------------------------------------------------ */
+
+/* SingleDimHistLayer (losses.py:40-57): hist[b][k] = inv_norm * sum_i phi_k(x[b][i]) over the
+ * m = C*H*W values of image b, K = 256 bins, L = 1/256, W = L/2.5 (inv_norm = 1/(C*H): the
+ * reference divides by x.size(1)*x.size(2)). hist [n][256] is overwritten. */
+int ast_soft_hist_f32(const float* x, int n, long long m, float inv_norm, float* hist, void* stream);
+
+/* EarthMoversDistanceLoss (losses.py:8-22) of two histograms [n][256], mean over n
+ * (compute_hist_loss, losses.py:84-87): *loss += weight * mean_b sum_t (cdf_x - cdf_y)^2;
+ * ghist [n][256] (may be NULL) = gscale * d/dhx. */
+int ast_emd_loss_f32(const float* hx, const float* hy, int n, float weight, const float* gscale,
+                     float* loss, float* ghist, void* stream);
+
+/* Backward of ast_soft_hist_f32: dx (+)= inv_norm * sum_k ghist[b][k] * dphi_k/dx. */
+int ast_soft_hist_backward_f32(const float* x, int n, long long m, float inv_norm,
+                               const float* ghist, float* dx, int accumulate, void* stream);
+
+/* out_of_range_loss (train.py:259): *loss += weight * mean huber(x - clip(x, 0, 1)) (the clipped
+ * copy is detached); dx (+)= its gradient. */
+int ast_range_loss_f32(const float* x, long long numel, float weight, const float* gscale,
+                       float* loss, float* dx, int accumulate, void* stream);
+
+/* *loss += weight * mean((x - y)^2) (org_img_loss pixel term, train.py:268); dx (+)= d/dx. */
+int ast_sqdiff_mean_f32(const float* x, const float* y, long long numel, float weight,
+                        const float* gscale, float* loss, float* dx, int accumulate, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

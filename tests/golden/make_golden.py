@@ -189,6 +189,7 @@ def main():
                         gram_grad=gram_grad.numpy(), style_loss=sl.detach().numpy(), style_grad=style_grad.numpy(),
                         content_loss=cl.detach().numpy(), content_grad=content_grad.numpy(),
                         img=img.detach().numpy(), tv=tv.detach().numpy(), tv_grad=img.grad.numpy())
+    hist_golden(R)
     train_step_golden(R, enc_wb, dec_wb)
     mobilenet_golden(R)
     adaattn_golden(R)
@@ -299,6 +300,25 @@ def adaattn_golden(R):
     np.savez_compressed(os.path.join(HERE, "adaattn.npz"), **out)
 
 
+def hist_golden(R):
+    """compute_hist_loss (losses.py:84-87) through the reference's module-level `hist` and
+    `earth_movers` instances: histograms, loss and d loss / d t_cs; plus the out_of_range term."""
+    L = R["_losses"]
+    x = torch.from_numpy((synth.uniform(821, 2 * 3 * 20 * 24) * 0.7 + 0.45).astype(np.float32).reshape(2, 3, 20, 24))
+    x.requires_grad_(True)
+    y = torch.from_numpy((synth.uniform(822, 2 * 3 * 20 * 24) * 0.5 + 0.5).astype(np.float32).reshape(2, 3, 20, 24))
+    hx, hy = L.hist(x.detach()), L.hist(y)
+    loss = L.compute_hist_loss(x, y)
+    loss.backward()
+    gx = x.grad.clone()
+    x.grad = None
+    r = L.compute_content_loss(x, torch.clip(x.detach(), 0.0, 1.0)) * 1e8      # train.py:259
+    r.backward()
+    np.savez_compressed(os.path.join(HERE, "hist.npz"), x=x.detach().numpy(), y=y.numpy(), hist_x=hx.numpy(),
+                        hist_y=hy.numpy(), loss=loss.detach().numpy(), grad=gx.numpy(),
+                        range_loss=r.detach().numpy(), range_grad=x.grad.numpy())
+
+
 def train_step_golden(R, enc_wb, dec_wb):
     """One AdaIN training step assembled from the reference's own functions
     exactly as train.py:191-300 assembles its losses: lifted PretrainedEncoder / AdaIN /
@@ -361,5 +381,7 @@ if __name__ == "__main__":
         mobilenet_golden(load_reference())
     elif "--adaattn" in sys.argv:
         adaattn_golden(load_reference())
+    elif "--hist" in sys.argv:
+        hist_golden(load_reference())
     else:
         main()

@@ -234,3 +234,22 @@ def test_attention_ast_oracle_matches_reference(golden):
     with torch.no_grad():
         y = R.mb_style_transfer(c, s, enc, dec, ada, exporting=True, att_sds=att)
     assert rel_inf(y, g["ast_out"]) < 1e-5
+
+
+def test_hist_oracle_matches_reference(golden):
+    """oracle.compute_hist_loss / soft_hist / out_of_range_loss vs the reference's losses.py
+    (module-level hist, earth_movers; train.py:259) incl. the input gradients."""
+    g = golden("hist")
+    x = torch.from_numpy(g["x"]).requires_grad_(True)
+    y = torch.from_numpy(g["y"])
+    assert rel_inf(R.soft_hist(x.detach()), g["hist_x"]) < 1e-6
+    assert rel_inf(R.soft_hist(y), g["hist_y"]) < 1e-6
+    loss = R.compute_hist_loss(x, y)
+    loss.backward()
+    assert abs(float(loss) - float(g["loss"])) <= 1e-6 * abs(float(g["loss"]))
+    assert rel_inf(x.grad, g["grad"]) < 1e-6
+    x.grad = None
+    r = R.out_of_range_loss(x)
+    r.backward()
+    assert abs(float(r) - float(g["range_loss"])) <= 1e-6 * abs(float(g["range_loss"]))
+    assert rel_inf(x.grad, g["range_grad"]) < 1e-6
