@@ -11,8 +11,14 @@ Per step (train.py:191-300, AdaIN version):
   tv      = tv_loss(stylised)                                      (:282)
   loss    = 1.25*content + 0.5*style + 1.0*lf + 6e-4*tv            (:283, defaults :416-425)
   Adam(lr 2e-4, betas (0.9, 0.999), eps 1e-5) after clip_grad_norm_(2.0, error_if_nonfinite).
-The hist / org_img / out_of_range terms of train.py:255-269 belong to the AdaAttN model and the
-histogram loss (SURVEY.md §8f "next") and are not part of this step.
+With `full_losses=True` (SURVEY.md §8f "next" #2) the step also carries the remaining terms of
+train.py:248-283, as the reference adds them to the loss:
+  org_out      = decoder(content features)                        (the AST's org_out, models.py:474)
+  org_img      = org_img_lam * (sum_i huber(lossnet(org_out)[i], content_map[i])
+                                + 100 * mean((content - org_out)^2))          (:248-256, :268-269)
+  out_of_range = 1e8 * huber(stylised, clip(stylised.detach(), 0, 1))          (:259)
+  hist         = 1e-5 * compute_hist_loss(stylised, style)                     (:261)
+  loss        += hist + org_img + out_of_range                                 (:283)
 
 Data parallel (config 4): one process per GPU, each with its own batch shard; decoder gradients
 land in one flat buffer and are averaged with a single all-reduce (RCCL over xGMI) before the
@@ -42,7 +48,7 @@ _RELU9 = 4
 
 def default_args(**kw):
     a = dict(train_iter=10, batch_size=8, lr=2e-4, content_lam=1.25, style_lam=0.5, tv_lam=0.0006, lf_lam=1.0,
-             save_dir="models/ast/", load=False, image_size=512)
+             org_img_lam=0.5, save_dir="models/ast/", load=False, image_size=512, full_losses=False)
     a.update(kw)
     return argparse.Namespace(**a)
 
@@ -98,8 +104,19 @@ class AdaINTrainer:
         content_loss = torch.stack(content_terms).sum()
         style_loss = torch.stack(style_terms).sum()
         loss = a.content_lam * content_loss + a.style_lam * style_loss + a.lf_lam * lf_loss + a.tv_lam * tv
-        return {"loss": loss, "content_loss": content_loss, "style_loss": style_loss, "lf_loss": lf_loss,
-                "tv_loss": tv, "stylized": stylized, "t": t}
+        out = {"loss": loss, "content_loss": content_loss, "style_loss": style_loss, "lf_loss": lf_loss,
+               "tv_loss": tv, "stylized": stylized, "t": t}
+        if getattr(a, "full_losses", False):
+            org_out = self.net.decoder(f_c)
+            o_taps = self.lossnet(org_out)
+            org_terms = [L.compute_content_loss(o_taps[j], content_map[i]) for i, j in enumerate(_LOSS_IDX)]
+            org_terms.append(L.pixel_mse_loss(org_out, content, 100.0))
+            org_img_loss = torch.stack(org_terms).sum() * a.org_img_lam
+            range_loss = L.out_of_range_loss(stylized, 1e8)
+            hist_loss = L.compute_hist_loss(stylized, style, 1e-5)
+            out["loss"] = loss + hist_loss + org_img_loss + range_loss
+            out.update(org_img_loss=org_img_loss, out_of_range_loss=range_loss, hist_loss=hist_loss, org_out=org_out)
+        return out
 
     def train_step(self, content, style, record=False):
         out = self.compute_losses(content, style)
@@ -112,7 +129,7 @@ class AdaINTrainer:
         if record:  # device -> host syncs, as train.py:302-306 does every step
             for k in ("content_loss", "style_loss", "lf_loss", "tv_loss"):
                 self.train_dict[k].append(float(out[k].item()))
-            self.train_dict["org_img_loss"].append(0.0)
+            self.train_dict["org_img_loss"].append(float(out["org_img_loss"].item()) if "org_img_loss" in out else 0.0)
         return out
 
     # ---- checkpoints (train.py:103-133) -------------------------------------------------------

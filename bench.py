@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--mode", choices=["fwd", "train", "mobilenet"], default="fwd",
                    help="fwd: config 2 (the headline metric); train: config 3/4 AdaIN training step; "
                         "mobilenet: config 5")
+    p.add_argument("--full-losses", action="store_true",
+                   help="train mode: add train.py's hist, org_img and out_of_range terms (SURVEY §8f next #2)")
     p.add_argument("--attention", action="store_true",
                    help="mobilenet mode: stylise with the reference AST's AdaAttN (SURVEY §8f next #1) "
                         "instead of AdaIN")
@@ -62,7 +64,7 @@ def train_bench(args, dev, rank, world):
     from arbitrarystyletransfer_amd.train import AdaINTrainer, default_args
     B, S = args.batch or 16, args.size or 512
     arena = None
-    trainer = AdaINTrainer(default_args(batch_size=B, image_size=S), device=dev)
+    trainer = AdaINTrainer(default_args(batch_size=B, image_size=S, full_losses=args.full_losses), device=dev)
     if world > 1:
         arena = dp.FlatGradArena(trainer.params)
         trainer.grad_hook = arena
@@ -101,7 +103,8 @@ def train_bench(args, dev, rank, world):
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (live-init weights, U[0,1) images), resident in HBM",
         "config": {"workload": f"AdaIN train step (decoder trained; VGG loss network to relu_15; content+style+"
-                               f"lf+tv losses; clip 2.0 + Adam), bs={B}/GPU {S}x{S} fp32",
+                               f"lf+tv{'+hist+org_img+out_of_range' if args.full_losses else ''} losses; "
+                               f"clip 2.0 + Adam), bs={B}/GPU {S}x{S} fp32",
                    "global_batch": B * world, "image_size": S, "parallelism": f"data-parallel x{world}"},
         "roofline": {"bound": "mfma", "kernel": "conv3x3 fwd/dgrad + wgrad MFMA launches of a step",
                      "achieved": tf, "peak": PEAK_FP32_MFMA_TF, "unit": "TFLOP/s", "frac": tf / PEAK_FP32_MFMA_TF,

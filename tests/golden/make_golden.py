@@ -191,6 +191,7 @@ def main():
                         img=img.detach().numpy(), tv=tv.detach().numpy(), tv_grad=img.grad.numpy())
     hist_golden(R)
     train_step_golden(R, enc_wb, dec_wb)
+    train_step_golden(R, enc_wb, dec_wb, full=True)
     mobilenet_golden(R)
     adaattn_golden(R)
     print("golden vectors written to", HERE)
@@ -319,7 +320,7 @@ def hist_golden(R):
                         range_loss=r.detach().numpy(), range_grad=x.grad.numpy())
 
 
-def train_step_golden(R, enc_wb, dec_wb):
+def train_step_golden(R, enc_wb, dec_wb, full=False):
     """One AdaIN training step assembled from the reference's own functions
     exactly as train.py:191-300 assembles its losses: lifted PretrainedEncoder / AdaIN /
     mean_variance_norm, the commented decoder spec, losses.py, torch Adam + clip_grad_norm_."""
@@ -341,7 +342,8 @@ def train_step_golden(R, enc_wb, dec_wb):
     style = torch.from_numpy(synth.image(812, (2, 3, 64, 64)))
 
     with torch.no_grad():
-        t = adain(enc(content)[0], enc(style)[0])
+        f_c = enc(content)[0]
+        t = adain(f_c, enc(style)[0])
     stylized = dec(t)
     content_map = lossnet(content)
     style_map = lossnet(style)
@@ -359,6 +361,20 @@ def train_step_golden(R, enc_wb, dec_wb):
     lf_loss = L.compute_content_loss(mvn(t), mvn(enc_stylized[0].detach()))                  # :276-277
     tv = L.tv_loss(stylized)                                                                 # :282
     loss = 1.25 * content_loss + 0.5 * style_loss + 1.0 * lf_loss + 0.0006 * tv             # :283
+    extra = {}
+    if full:   # the remaining terms of train.py:248-283 (org_out = decoder(content features))
+        org_out = dec(f_c)
+        org_out_map = lossnet(org_out)
+        for i in range(len(org_out_map)):                                                  # :248-256
+            term = L.compute_content_loss(org_out_map[i], content_map[i].detach())
+            org_img_loss = term if i == 0 else org_img_loss + term
+        out_of_range_loss = L.compute_content_loss(stylized, torch.clip(stylized.detach(), 0.0, 1.0)) * 1e8  # :259
+        hist_loss = L.compute_hist_loss(stylized, style) * 1e-5                           # :261
+        org_img_loss = org_img_loss + ((content.detach() - org_out) ** 2).mean() * 100    # :268
+        org_img_loss = org_img_loss * 0.5                                                 # :270 (org_img_lam)
+        loss = loss + hist_loss + org_img_loss + out_of_range_loss                        # :283
+        extra = dict(org_out=org_out.detach().numpy(), org_img_loss=org_img_loss.detach().numpy(),
+                     hist_loss=hist_loss.detach().numpy(), out_of_range_loss=out_of_range_loss.detach().numpy())
     opt.zero_grad()
     loss.backward()
     grads = [p.grad.detach().clone() for p in dec.parameters()]
@@ -367,12 +383,12 @@ def train_step_golden(R, enc_wb, dec_wb):
     out = dict(content=content.numpy(), style=style.numpy(), stylized=stylized.detach().numpy(),
                content_loss=content_loss.detach().numpy(), style_loss=style_loss.detach().numpy(),
                lf_loss=lf_loss.detach().numpy(), tv_loss=tv.detach().numpy(), loss=loss.detach().numpy(),
-               grad_norm=norm.detach().numpy())
+               grad_norm=norm.detach().numpy(), **extra)
     for i, (g, p) in enumerate(zip(grads, dec.parameters())):
         out[f"grad{i}"] = g.numpy() if g.numel() <= 4096 else g.reshape(-1)[::97].numpy()
         out[f"grad{i}_sum"] = np.array([g.double().sum().item(), g.double().abs().sum().item()])
         out[f"param{i}"] = p.detach().numpy() if p.numel() <= 4096 else p.detach().reshape(-1)[::97].numpy()
-    np.savez_compressed(os.path.join(HERE, "train_step_64.npz"), **out)
+    np.savez_compressed(os.path.join(HERE, "train_step_full_64.npz" if full else "train_step_64.npz"), **out)
 
 
 if __name__ == "__main__":
@@ -383,5 +399,7 @@ if __name__ == "__main__":
         adaattn_golden(load_reference())
     elif "--hist" in sys.argv:
         hist_golden(load_reference())
+    elif "--train-full" in sys.argv:
+        train_step_golden(load_reference(), synth.vgg_encoder_weights(1), synth.vgg_decoder_weights(2), full=True)
     else:
         main()

@@ -290,3 +290,52 @@ def test_dp_arena_adopts_kernel_gradients(hip_device):
         assert torch.isfinite(arena.flat).all()
     finally:
         arena.unregister()
+
+
+def test_train_step_full_losses_golden(golden, hip_device):
+    """The full train.py:191-300 loss (content, style, lf, tv + hist, org_img, out_of_range;
+    SURVEY.md §8f "next" #2) against the reference's own step (train_step_full_64.npz), with the
+    gradient compared conditioning-free as in test_train_step_golden."""
+    from arbitrarystyletransfer_amd.train import AdaINTrainer, default_args
+    g = golden("train_step_full_64")
+    d = hip_device
+    snap = {}
+
+    def hook(params):
+        snap["grads"] = [p.grad.detach().clone() for p in params]
+
+    tr = AdaINTrainer(default_args(batch_size=2, full_losses=True), device=d, grad_hook=hook)
+    content, style = torch.from_numpy(g["content"]), torch.from_numpy(g["style"])
+    out = tr.train_step(content.to(d), style.to(d))
+    for k in ("content_loss", "style_loss", "lf_loss", "tv_loss", "hist_loss", "org_img_loss",
+              "out_of_range_loss", "loss"):
+        np.testing.assert_allclose(out[k].item(), float(g[k]), rtol=1e-4, err_msg=k)
+    assert rel_inf(out["stylized"], g["stylized"]) <= 1e-4
+    assert rel_inf(out["org_out"], g["org_out"]) <= 1e-4
+    np.testing.assert_allclose(out["grad_norm"].item(), float(g["grad_norm"]), rtol=2e-2)
+
+    enc = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_encoder_weights(1)]
+    dec = [(torch.from_numpy(w).clone().requires_grad_(), torch.from_numpy(b).clone().requires_grad_())
+           for w, b in synth.vgg_decoder_weights(2)]
+    xs = out["stylized"].detach().cpu().requires_grad_()
+    xo = out["org_out"].detach().cpu().requires_grad_()
+    names = R.LOSSNET_LAYERS
+    cm = [m.detach() for m in R.vgg_encoder(content, enc, names)]
+    sm = [m.detach() for m in R.vgg_encoder(style, enc, names)]
+    tcs = R.vgg_encoder(xs, enc, names)
+    om = R.vgg_encoder(xo, enc, names)
+    cl = sum(R.compute_content_loss(R.mean_variance_norm(a), R.mean_variance_norm(b)) for a, b in zip(tcs, cm))
+    cl = cl + R.compute_content_loss(R.mean_variance_norm(xs), R.mean_variance_norm(content)) * 0.1
+    sl = sum(R.compute_style_loss(a, b) * w for a, b, w in zip(tcs, sm, R.STYLE_WEIGHTS))
+    sl = sl + R.compute_style_loss(xs, style)
+    org = (sum(R.compute_content_loss(a, b) for a, b in zip(om, cm)) + ((content - xo) ** 2).mean() * 100) * 0.5
+    total = (1.25 * cl + 0.5 * sl + 0.0006 * R.tv_loss(xs) + R.compute_hist_loss(xs, style) * 1e-5
+             + org + R.out_of_range_loss(xs))
+    total.backward()
+    t = out["t"].detach().cpu()
+    f_c = torch.from_numpy(g["content"])
+    f_c = R.vgg_encoder(f_c, enc, ["relu_9"])[0]
+    params = [p for wb in dec for p in wb]
+    torch.autograd.backward([R.vgg_decoder(t, dec), R.vgg_decoder(f_c, dec)], grad_tensors=[xs.grad, xo.grad])
+    for i, (gr, p) in enumerate(zip(snap["grads"], params)):
+        assert rel_inf(gr, p.grad) <= 2e-4, (i, rel_inf(gr, p.grad))
