@@ -38,6 +38,7 @@ __device__ __forceinline__ float ld(const __bf16* p) { return (float)*p; }
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -389,56 +390,80 @@ struct ProjB16Args {
   int n, C, Cp, nq, nk, nqp, nkp;
 };
 
+// bf16 projections on v_mfma_f32_32x32x16_bf16. Workgroup = 4 waves x 32 pixels. The input tile
+// [C][128 px] is read with 16-byte loads, normalised in fp32 ((x - mean) * rstd for Q/K, x - mean
+// for V) and written to LDS pixel-major as bf16 (xs[px][CK + 8]); W is staged as bf16
+// ws[o][CK + 8] (CK = C rounded to 16, zero padded). A fragment = 8 consecutive channels of one
+// row of either image (16-byte, conflict-free reads). Q/K: D[pixel][o] (lane = o: 64-byte rows
+// of the pixel-major output); V: D[o][pixel] (lane = pixel) plus V^2 from the fp32 accumulator.
 template <int CT>
 __global__ __launch_bounds__(256) void project_bf16_kernel(ProjB16Args a) {
-  extern __shared__ float wt[];  // [C_even][Cp + 32]
+  extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
   const int which = blockIdx.z;  // 0 = q, 1 = k, 2 = v (+ v2)
   const int b = blockIdx.y;
   const int N = which == 0 ? a.nq : a.nk;
   const int Np = which == 0 ? a.nqp : a.nkp;
   const int p0 = blockIdx.x * 128;
   if (p0 >= Np) return;
-  const int C = a.C, Cp = a.Cp, ce = (C + 1) & ~1, pitch = Cp + 32;
+  constexpr int CP = CT * 32;
+  const int C = a.C, CK = (C + 15) & ~15, RP = CK + 8;
+  bf16* xs = reinterpret_cast<bf16*>(psm);  // [128][RP]
+  bf16* ws = xs + 128 * RP;                 // [CP][RP]
   const float* __restrict__ w = which == 0 ? a.wq : (which == 1 ? a.wk : a.wv);
-  for (int i = threadIdx.x; i < ce * Cp; i += 256) {
-    const int c = i / Cp, o = i - c * Cp;
-    wt[c * pitch + o] = (c < C && o < C) ? w[(int64_t)o * C + c] : 0.f;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < CP * CK; i += 256) {
+    const int o = i / CK, c = i - o * CK;
+    ws[o * RP + c] = (bf16)((o < C && c < C) ? w[(int64_t)o * C + c] : 0.f);
+  }
+  const bf16* __restrict__ x = (which == 0 ? a.c : a.s) + (int64_t)b * C * N;
+  const float* mean = (which == 0 ? a.stats : a.stats + 2 * (int64_t)a.n * C) + (int64_t)b * C;
+  const float* rstd = mean + (int64_t)a.n * C;
+  const bool scale = which != 2;
+  // Q carries the softmax's log2(e) (scores come out in log2 units: exp2 without a multiply)
+  const float qs = which == 0 ? kLog2e : 1.f;
+  // 16 pieces of 8 pixels per channel row; vector loads when the row is 16-byte aligned
+  const bool vec = (N % 8) == 0;
+  for (int i = tid; i < CK * 16; i += 256) {
+    const int c = i >> 4, q = (i & 15) * 8, px = p0 + q;
+    float v[8];
+    if (c < C) {
+      const float m = mean[c], rs = (scale ? rstd[c] : 1.f) * qs;
+      const bf16* xr = x + (int64_t)c * N;
+      if (vec && px + 8 <= N) {
+        const bf16x8 t = *reinterpret_cast<const bf16x8*>(xr + px);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = ((float)t[j] - m) * rs;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = px + j < N ? ((float)xr[px + j] - m) * rs : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xs[(q + j) * RP + c] = (bf16)v[j];
   }
   __syncthreads();
 
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int px = p0 + wv * 32 + r;
-  const bf16* __restrict__ x = (which == 0 ? a.c : a.s) + (int64_t)b * C * N;
-  const float* mean = which == 0 ? a.stats : a.stats + 2 * (int64_t)a.n * C;
-  const float* rstd = mean + (int64_t)a.n * C;
-  mean += (int64_t)b * C;
-  rstd += (int64_t)b * C;
-  const bool pin = px < N, pm = which == 0 ? false : true;
-  (void)pm;
-
+  const int lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
   f32x16 acc[CT];
 #pragma unroll
   for (int t = 0; t < CT; ++t) acc[t] = (f32x16){0.f};
-  for (int m = 0; m < ce / 2; ++m) {
-    const int c = 2 * m + h;
-    float xv = 0.f;
-    if (pin && c < C) {
-      xv = (float)x[(int64_t)c * N + px] - mean[c];
-      if (which != 2) xv *= rstd[c];
-    }
-    const float* wr = wt + c * pitch + r;
-    if (which == 2) {  // D[o][pixel]: lane = pixel
+  const bf16* xrow = xs + (wv * 32 + r) * RP + 8 * h;
+  for (int k0 = 0; k0 < CK; k0 += 16) {
+    const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xrow + k0);
 #pragma unroll
-      for (int t = 0; t < CT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[t * 32], xv, acc[t], 0, 0, 0);
-    } else {           // D[pixel][o]: lane = output channel
-#pragma unroll
-      for (int t = 0; t < CT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(xv, wr[t * 32], acc[t], 0, 0, 0);
+    for (int t = 0; t < CT; ++t) {
+      const bf16x8 wf = *reinterpret_cast<const bf16x8*>(ws + (t * 32 + r) * RP + 8 * h + k0);
+      acc[t] = which == 2 ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xf, acc[t], 0, 0, 0)
+                          : __builtin_amdgcn_mfma_f32_32x32x16_bf16(xf, wf, acc[t], 0, 0, 0);
     }
   }
   const int pw0 = p0 + wv * 32;
   if (which == 2) {
-    bf16* __restrict__ y = a.v + (int64_t)b * Cp * Np;
-    bf16* __restrict__ y2 = a.v2 + (int64_t)b * Cp * Np;
+    bf16* __restrict__ y = a.v + (int64_t)b * CP * Np;
+    bf16* __restrict__ y2 = a.v2 + (int64_t)b * CP * Np;
     const int pw = pw0 + r;
     if (pw < Np) {
 #pragma unroll
@@ -452,13 +477,13 @@ __global__ __launch_bounds__(256) void project_bf16_kernel(ProjB16Args a) {
         }
     }
   } else {
-    bf16* __restrict__ y = (which == 0 ? a.q : a.k) + (int64_t)b * Np * Cp;
+    bf16* __restrict__ y = (which == 0 ? a.q : a.k) + (int64_t)b * Np * CP;
 #pragma unroll
     for (int t = 0; t < CT; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int p = pw0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (p < Np) y[(int64_t)p * Cp + t * 32 + r] = (bf16)acc[t][i];
+        if (p < Np) y[(int64_t)p * CP + t * 32 + r] = (bf16)acc[t][i];
       }
   }
 }
@@ -491,13 +516,15 @@ struct AttnB16Args {
 //   S^T = K Q^T: A = K from LDS ([key][Cp + 8] bf16 rows: 16-byte reads, conflict-free), B = this
 //   lane's Q fragment (registers, loaded once).
 //   P = bf16(exp2(S - m)) straight from the accumulator: registers 8s..8s+7 are the B fragment of
-//   k-step s with key order 16s + 8(j>>2) + 4h + (j&3); the A operand (V^T) is read in that same
-//   key order as two 8-byte reads from [ch][36] rows (72-byte pitch: conflict-free).
+//   k-step s with key order 16s + 8(j>>2) + 4h + (j&3). V and V^2 rows ([ch][40] bf16, 80-byte
+//   pitch) store each 16-key group in exactly that order (keys 0-3, 8-11, 4-7, 12-15), so the A
+//   operand (V^T) is one conflict-free 16-byte read (ds_read_b128: 256 B/clk, vs 128 for the
+//   ds_read2_b64 pair a natural key order needs).
 constexpr int KPB = 8;   // K row padding (bf16)
-constexpr int VPB = 36;  // V row pitch (bf16)
+constexpr int VPB = 40;  // V row pitch (bf16): 20 dwords, distinct bank quads per b128 lane group
 
-template <int CT>
-__global__ __launch_bounds__(512, 1) void attend_bf16_kernel(AttnB16Args a) {
+template <int CT, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attend_bf16_kernel(AttnB16Args a) {
   constexpr int CP = CT * 32, KROW = CP + KPB;
   __shared__ __attribute__((aligned(16))) bf16 ks[2][BK * KROW];
   __shared__ __attribute__((aligned(16))) bf16 vs[2][CP * VPB];
@@ -505,7 +532,7 @@ __global__ __launch_bounds__(512, 1) void attend_bf16_kernel(AttnB16Args a) {
   int b, tile;
   map_tile(blockIdx.x, gridDim.x, a.qtiles, b, tile);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int qi = tile * 256 + wv * 32 + r;
+  const int qi = tile * (NW * 32) + wv * 32 + r;
 
   bf16x8 qf[CP / 16];
   {
@@ -513,35 +540,48 @@ __global__ __launch_bounds__(512, 1) void attend_bf16_kernel(AttnB16Args a) {
 #pragma unroll
     for (int s = 0; s < CP / 16; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
   }
+  // Retire the Q loads here: otherwise the compiler's wait-count placement waits for them inside
+  // the loop, where the same waits then also drain every block's K/V prefetch.
+  __builtin_amdgcn_s_waitcnt(0);
 
   // staging: K block = 32 rows x CP bf16 (CP/8 16-byte pieces per row); V, V2 blocks = CP rows x
   // 32 keys (4 pieces per row). One piece of each per thread (CP = 128), fewer threads otherwise.
   const bf16* __restrict__ kb = a.k + (int64_t)b * a.nkp * CP;
   const bf16* __restrict__ vb = a.v + (int64_t)b * CP * a.nkp;
   const bf16* __restrict__ v2b = a.v2 + (int64_t)b * CP * a.nkp;
-  constexpr int NPIECE = CP * 4;  // = 32 * CP / 8
-  const bool stager = tid < NPIECE;
-  const int krow = tid / (CP / 8), kcol = (tid % (CP / 8)) * 8;
-  const int vrow = tid >> 2, vcol = (tid & 3) * 8;
+  constexpr int NT = NW * 64, NPIECE = CP * 4;  // 16-byte pieces per block of each of K, V, V2
+  constexpr int PPT = (NPIECE + NT - 1) / NT;
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-  u32x4 kr = {0, 0, 0, 0}, vr = kr, v2r = kr;
+  u32x4 kr[PPT], vr[PPT], v2r[PPT];
   auto gload = [&](int kbase) {
-    if (stager) {
-      kr = *reinterpret_cast<const u32x4*>(kb + (int64_t)(kbase + krow) * CP + kcol);
-      vr = *reinterpret_cast<const u32x4*>(vb + (int64_t)vrow * a.nkp + kbase + vcol);
-      v2r = *reinterpret_cast<const u32x4*>(v2b + (int64_t)vrow * a.nkp + kbase + vcol);
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int e = tid + i * NT;
+      if (NPIECE % NT == 0 || e < NPIECE) {
+        const int krow = e / (CP / 8), kcol = (e % (CP / 8)) * 8, vrow = e >> 2, vcol = (e & 3) * 8;
+        kr[i] = *reinterpret_cast<const u32x4*>(kb + (int64_t)(kbase + krow) * CP + kcol);
+        vr[i] = *reinterpret_cast<const u32x4*>(vb + (int64_t)vrow * a.nkp + kbase + vcol);
+        v2r[i] = *reinterpret_cast<const u32x4*>(v2b + (int64_t)vrow * a.nkp + kbase + vcol);
+      }
     }
   };
   auto lstore = [&](int buf) {
-    if (stager) {
-      *reinterpret_cast<u32x4*>(&ks[buf][krow * KROW + kcol]) = kr;
-      u32x2* pv = reinterpret_cast<u32x2*>(&vs[buf][vrow * VPB + vcol]);
-      pv[0] = (u32x2){vr[0], vr[1]};
-      pv[1] = (u32x2){vr[2], vr[3]};
-      u32x2* pv2 = reinterpret_cast<u32x2*>(&v2s[buf][vrow * VPB + vcol]);
-      pv2[0] = (u32x2){v2r[0], v2r[1]};
-      pv2[1] = (u32x2){v2r[2], v2r[3]};
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int e = tid + i * NT;
+      if (NPIECE % NT == 0 || e < NPIECE) {
+        const int krow = e / (CP / 8), kcol = (e % (CP / 8)) * 8, vrow = e >> 2, vcol = (e & 3) * 8;
+        *reinterpret_cast<u32x4*>(&ks[buf][krow * KROW + kcol]) = kr[i];
+        // keys vcol..vcol+7 (vcol = 8u): first 4 to slot 16(u>>1) + 4(u&1), last 4 eight slots later
+        const int u = vcol >> 3, slot = 16 * (u >> 1) + 4 * (u & 1);
+        bf16* pv = &vs[buf][vrow * VPB + slot];
+        *reinterpret_cast<u32x2*>(pv) = (u32x2){vr[i][0], vr[i][1]};
+        *reinterpret_cast<u32x2*>(pv + 8) = (u32x2){vr[i][2], vr[i][3]};
+        bf16* pv2 = &v2s[buf][vrow * VPB + slot];
+        *reinterpret_cast<u32x2*>(pv2) = (u32x2){v2r[i][0], v2r[i][1]};
+        *reinterpret_cast<u32x2*>(pv2 + 8) = (u32x2){v2r[i][2], v2r[i][3]};
+      }
     }
   };
 
@@ -551,7 +591,8 @@ __global__ __launch_bounds__(512, 1) void attend_bf16_kernel(AttnB16Args a) {
     om[t] = (f32x16){0.f};
     osq[t] = (f32x16){0.f};
   }
-  float mrow = -INFINITY, lsum = 0.f;
+  float mrow = -INFINITY;
+  f32x2 lsum2 = {0.f, 0.f};
   const int nblk = a.nkp / BK;
   gload(0);
   lstore(0);
@@ -560,13 +601,19 @@ __global__ __launch_bounds__(512, 1) void attend_bf16_kernel(AttnB16Args a) {
     if (j + 1 < nblk) gload((j + 1) * BK);
     __syncthreads();
 
-    f32x16 s = (f32x16){0.f};
+    // S^T in log2 units (Q carries log2 e); two independent accumulation chains (a 32x32x16
+    // MFMA's dependent latency is twice its issue interval)
+    f32x16 s0 = (f32x16){0.f}, s1 = (f32x16){0.f};
     const bf16* kk = &ks[buf][r * KROW + 8 * h];
 #pragma unroll
-    for (int st = 0; st < CP / 16; ++st)
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(kk + 16 * st), qf[st], s, 0, 0, 0);
-    s *= kLog2e;
-    {
+    for (int st = 0; st < CP / 16; st += 2) {
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(kk + 16 * st), qf[st], s0, 0, 0, 0);
+      if (st + 1 < CP / 16)
+        s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(kk + 16 * st + 16), qf[st + 1],
+                                                     s1, 0, 0, 0);
+    }
+    f32x16 s = s0 + s1;
+    if (j * BK + BK > a.nk) {  // last block only (wave-uniform)
       const int lim = a.nk - j * BK - 4 * h;
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2) < lim) ? s[i] : -INFINITY;
@@ -578,7 +625,7 @@ __global__ __launch_bounds__(512, 1) void attend_bf16_kernel(AttnB16Args a) {
     if (__builtin_expect(__ballot(mb > mrow + kRescaleLog2) != 0, 0)) {
       const float mnew = fmaxf(mrow, mb);
       const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
-      lsum *= alpha;
+      lsum2 *= alpha;
 #pragma unroll
       for (int t = 0; t < CT; ++t) {
         om[t] *= alpha;
@@ -588,24 +635,26 @@ __global__ __launch_bounds__(512, 1) void attend_bf16_kernel(AttnB16Args a) {
       mrow = mnew;
     }
     bf16x8 pb[2];
+    {
+      const f32x2 m2 = {mrow, mrow};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const bf16 pv = (bf16)__builtin_amdgcn_exp2f(s[i] - mrow);
-      lsum += (float)pv;  // normalise by the weights actually applied
-      pb[i >> 3][i & 7] = pv;
+      for (int i = 0; i < 16; i += 2) {
+        f32x2 d = (f32x2){s[i], s[i + 1]} - m2;
+        d[0] = __builtin_amdgcn_exp2f(d[0]);
+        d[1] = __builtin_amdgcn_exp2f(d[1]);
+        lsum2 += d;
+        pb[i >> 3][i & 7] = (bf16)d[0];
+        pb[i >> 3][(i & 7) + 1] = (bf16)d[1];
+      }
     }
 
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
 #pragma unroll
       for (int t = 0; t < CT; ++t) {
-        const int off = (t * 32 + r) * VPB + 16 * st + 4 * h;
-        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(&vs[buf][off]);
-        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(&vs[buf][off + 8]);
-        const bf16x4 lo2 = *reinterpret_cast<const bf16x4*>(&v2s[buf][off]);
-        const bf16x4 hi2 = *reinterpret_cast<const bf16x4*>(&v2s[buf][off + 8]);
-        const bf16x8 va = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        const bf16x8 va2 = __builtin_shufflevector(lo2, hi2, 0, 1, 2, 3, 4, 5, 6, 7);
+        const int off = (t * 32 + r) * VPB + 16 * st + 8 * h;
+        const bf16x8 va = *reinterpret_cast<const bf16x8*>(&vs[buf][off]);
+        const bf16x8 va2 = *reinterpret_cast<const bf16x8*>(&v2s[buf][off]);
         om[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb[st], om[t], 0, 0, 0);
         osq[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va2, pb[st], osq[t], 0, 0, 0);
       }
@@ -614,6 +663,7 @@ __global__ __launch_bounds__(512, 1) void attend_bf16_kernel(AttnB16Args a) {
   }
 
   if (qi >= a.nq) return;
+  const float lsum = lsum2[0] + lsum2[1];
   const float inv = 1.0f / (lsum + __shfl_xor(lsum, 32, 64));
   const float* cmean = a.stats + (int64_t)b * a.C;
   const float* crstd = a.stats + (int64_t)a.n * a.C + (int64_t)b * a.C;
@@ -728,13 +778,22 @@ int ast_adaattn_fwd(int dtype, const void* content, const void* style, const flo
   ProjB16Args pa{(const bf16*)content, (const bf16*)style, wq, wk, wv, stats, q, k, v, v2, n, c, cp, nq, nk, nqp, nkp};
   void (*proj)(ProjB16Args) = ct == 1 ? project_bf16_kernel<1> : ct == 2 ? project_bf16_kernel<2>
                             : ct == 3 ? project_bf16_kernel<3> : project_bf16_kernel<4>;
-  if ((e = set_lds(proj, plds)) != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(proj, pgrid, dim3(256), plds, st, pa);
-  const int qtiles = nqp / 256;
+  const size_t plds16 = 2 * (size_t)(128 + cp) * (((c + 15) & ~15) + 8);
+  if ((e = set_lds(proj, plds16)) != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(proj, pgrid, dim3(256), plds16, st, pa);
+  // 8 waves (256 queries) per workgroup: each K/V block staged in LDS serves 256 queries. Small
+  // problems (< 512 such workgroups) use 4-wave workgroups instead, to spread over more CUs.
+  const bool big = (int64_t)n * (nqp / 256) >= 512;
+  const int nw = big ? 8 : 4, qtiles = nqp / (nw * 32);
   AttnB16Args aa{q, k, v, v2, (const bf16*)content, stats, vmean, (bf16*)out, n, c, cp, nq, nk, nqp, nkp, qtiles};
-  void (*att)(AttnB16Args) = ct == 1 ? attend_bf16_kernel<1> : ct == 2 ? attend_bf16_kernel<2>
-                           : ct == 3 ? attend_bf16_kernel<3> : attend_bf16_kernel<4>;
-  hipLaunchKernelGGL(att, dim3((unsigned)(n * qtiles)), dim3(512), 0, st, aa);
+  void (*att)(AttnB16Args);
+  if (big)
+    att = ct == 1 ? attend_bf16_kernel<1, 8> : ct == 2 ? attend_bf16_kernel<2, 8> : ct == 3 ? attend_bf16_kernel<3, 8>
+                                                                                    : attend_bf16_kernel<4, 8>;
+  else
+    att = ct == 1 ? attend_bf16_kernel<1, 4> : ct == 2 ? attend_bf16_kernel<2, 4> : ct == 3 ? attend_bf16_kernel<3, 4>
+                                                                                    : attend_bf16_kernel<4, 4>;
+  hipLaunchKernelGGL(att, dim3((unsigned)(n * qtiles)), dim3(nw * 64), 0, st, aa);
   return (int)hipGetLastError();
 }
 

@@ -31,6 +31,12 @@ def run(n, c, h, w, dtype=torch.float32, iters=5):
 
 
 if __name__ == "__main__":
+    if "--big-bf16" in sys.argv:   # one config-5-sized call (PMC runs)
+        run(32, 128, 128, 128, torch.bfloat16, iters=1)
+        sys.exit(0)
+    if "--big-f32" in sys.argv:
+        run(32, 128, 128, 128, torch.float32, iters=1)
+        sys.exit(0)
     dts = [torch.float32] + ([torch.bfloat16] if "--bf16" in sys.argv else [])
     for dt in dts:
         run(1, 128, 64, 64, dt)
