@@ -17,6 +17,7 @@
 // workgroups). dY may be read from the padded gradient buffer (pitch/plane/offset).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "../../include/ast_hip.h"
 
 namespace {
@@ -307,6 +308,144 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgArgs a) {
   if (a.db && cig == 0 && co0 + (tid & 63) < a.Cout) atomicAdd(a.db + co0 + (tid & 63), bacc);
 }
 
+// Aligned-shape weight gradient (Cin, Cout multiples of 64; output W a multiple of 32, H even):
+// the same tile, LDS images and MFMA loop as wgrad_kernel, with the staging rebuilt around a
+// register prefetch -- the next tile's input halo (float4 pieces, halo columns as single floats)
+// and dY are loaded while the current tile's MFMAs run, from per-thread offsets computed once.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int UP>
+__global__ __launch_bounds__(256, 2) void wgrad2_kernel(WgArgs a) {
+  using C = WgCfg<UP>;
+  constexpr int SW = C::SW, SR = C::SR, RS = C::RS, PS = C::PS, QV = C::QV, C0 = C::C0;
+  constexpr int NI = WG_CI * SR * QV;        // float4 input pieces per tile
+  constexpr int KI = (NI + 255) / 256;
+  constexpr int NH = WG_CI * SR * 2;         // halo columns per tile
+  constexpr int KH = (NH + 255) / 256;
+  constexpr int KD = WG_CO * WG_PIX / 256;   // dY values per thread (16)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Ps = smem;                   // [WG_CI][PS]
+  float* Ds = smem + WG_CI * PS;      // [WG_PIX][WG_DS]
+  const int Hin = a.Hin, Win = a.Win;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int wco = wave & 1, wci = wave >> 1;
+  const int co_groups = a.Cout / WG_CO, ci_groups = a.Cin / WG_CI;
+  int b = blockIdx.x;
+  const int cog = b % co_groups;
+  b /= co_groups;
+  const int cig = b % ci_groups;
+  const int split = b / ci_groups;
+  const int co0 = cog * WG_CO, ci0 = cig * WG_CI;
+  const int plane_in = Hin * Win;
+
+  // staging items (recomputed where used, constant divisors): float4 piece e = tid + 256k ->
+  // (channel, halo row, column q); halo item -> (channel, row, left/right)
+#define WG2_ITEM(k)                                                      \
+  const int e_ = min(tid + 256 * (k), NI - 1);                           \
+  const int q_ = e_ % QV, cr_ = e_ / QV, r_ = cr_ % SR, c_ = cr_ / SR;
+#define WG2_HALO(k)                                                      \
+  const int e_ = min(tid + 256 * (k), NH - 1);                           \
+  const int s_ = e_ & 1, cr_ = e_ >> 1, r_ = cr_ % SR, c_ = cr_ / SR;
+  const int d_pix = tid & 63, d_c = tid >> 6;
+  const int d_off = (d_pix / WG_TW) * a.dy_pitch + d_pix % WG_TW;
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = (f32x16){0.f};
+  float bacc = 0.f;
+  int bcol[3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) bcol[kx] = (UP == 1) ? (C0 - 1 + h + kx) : (C0 + ((h + kx - 1) >> 1));
+  const float* prow_base = Ps + (wci * 32 + l32) * PS;
+  const int arow = wco * 32 + l32;
+
+  f32x4 xr[KI];
+  float hr[KH];
+  float dr[KD];
+  auto load_tile = [&](int tile) {
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int n = tt / a.tiles_y;
+    const int x0 = tx * WG_TW, y0 = ty * WG_TH;
+    const int sx0 = x0 / UP, sy0 = y0 / UP - 1;
+    const float* xin = a.x + (int64_t)n * a.Cin * plane_in;
+    const int sxl = src_index<UP>(sx0 - 1, Win, a.reflect), sxr = src_index<UP>(sx0 + SW, Win, a.reflect);
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      WG2_ITEM(k)
+      const int sy = src_index<UP>(sy0 + r_, Hin, a.reflect);
+      xr[k] = sy >= 0 ? *reinterpret_cast<const f32x4*>(xin + (ci0 + c_) * plane_in + sy * Win + sx0 + 4 * q_)
+                      : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < KH; ++k) {
+      WG2_HALO(k)
+      const int sy = src_index<UP>(sy0 + r_, Hin, a.reflect), sx = s_ ? sxr : sxl;
+      hr[k] = (sy >= 0 && sx >= 0) ? xin[(ci0 + c_) * plane_in + sy * Win + sx] : 0.f;
+    }
+    const float* dyn = a.dy + (int64_t)n * a.Cout * a.dy_plane + a.dy_off + (int64_t)y0 * a.dy_pitch + x0 + d_off +
+                       (int64_t)(co0 + d_c) * a.dy_plane;
+#pragma unroll
+    for (int k = 0; k < KD; ++k) dr[k] = dyn[(int64_t)(4 * k) * a.dy_plane];
+  };
+
+  const int t0 = (int)(a.tiles_per_block * split);
+  const int t1 = (int)min(a.ntiles, (int64_t)t0 + a.tiles_per_block);
+  if (t0 < t1) load_tile(t0);
+  for (int tile = t0; tile < t1; ++tile) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      WG2_ITEM(k)
+      float* d = Ps + c_ * PS + r_ * RS + C0 + 4 * q_;
+      d[0] = xr[k][0]; d[1] = xr[k][1]; d[2] = xr[k][2]; d[3] = xr[k][3];
+    }
+#pragma unroll
+    for (int k = 0; k < KH; ++k) {
+      WG2_HALO(k)
+      Ps[c_ * PS + r_ * RS + (s_ ? C0 + SW : C0 - 1)] = hr[k];
+    }
+#pragma unroll
+    for (int k = 0; k < KD; ++k) Ds[d_pix * WG_DS + d_c + 4 * k] = dr[k];
+    __syncthreads();
+    if (tile + 1 < t1) load_tile(tile + 1);
+    if (a.db && cig == 0) {
+      const int c = tid & 63, q = tid >> 6;
+#pragma unroll
+      for (int k = 0; k < WG_PIX / 4; ++k) bacc += Ds[(q * (WG_PIX / 4) + k) * WG_DS + c];
+    }
+#pragma unroll 2
+    for (int kp = 0; kp < WG_PIX / 2; ++kp) {
+      const int prow = (2 * kp) / WG_TW;
+      const int pc0 = (2 * kp) % WG_TW;
+      const float av = Ds[(2 * kp + h) * WG_DS + arow];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int srow = (UP == 1) ? prow + ky : ((prow + ky - 1) >> 1) + 1;
+        const float* rp = prow_base + srow * RS + ((UP == 1) ? pc0 : (pc0 >> 1));
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+          acc[ky * 3 + kx] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, rp[bcol[kx]], acc[ky * 3 + kx], 0, 0, 0);
+      }
+    }
+  }
+  const int ci = ci0 + wci * 32 + l32;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      atomicAdd(a.dw + ((int64_t)co * a.Cin + ci) * 9 + t, acc[t][r]);
+    }
+  if (a.db && cig == 0) atomicAdd(a.db + co0 + (tid & 63), bacc);
+#undef WG2_ITEM
+#undef WG2_HALO
+}
+
+int g_wgrad_v1 = 0;  // AST_WGRAD_V1=1: always the general kernel (A/B measurements)
+
 int grid1(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 inline int round_up(int a, int b) { return cdiv(a, b) * b; }
@@ -382,6 +521,11 @@ int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* 
   }
   if (dy_pitch < W || dy_plane < (long long)H * dy_pitch || dy_offset < 0) return AST_E_SHAPE;
   hipStream_t s = (hipStream_t)stream;
+  static const int v1 = [] {
+    const char* v = getenv("AST_WGRAD_V1");
+    return v ? atoi(v) : 0;
+  }();
+  g_wgrad_v1 = v1;
   hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * (size_t)cout * cin * 9, s);
   if (e != hipSuccess) return (int)e;
   if (db) {
@@ -402,7 +546,14 @@ int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* 
   splits = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
   const int64_t nblk = splits * groups;
   if (nblk >= 0x7fffffff) return AST_E_SHAPE;
-  if (upsample == 2)
+  const bool aligned = cin % WG_CI == 0 && cout % WG_CO == 0 && W % WG_TW == 0 && H % WG_TH == 0 && w_in % 4 == 0 &&
+                       a.ntiles < 0x7fffffff && (int64_t)n * cin * h_in * w_in < 0x7fffffffLL &&
+                       (int64_t)cout * dy_plane < 0x7fffffffLL && !g_wgrad_v1;
+  if (aligned && upsample == 2)
+    hipLaunchKernelGGL(wgrad2_kernel<2>, dim3((unsigned)nblk), dim3(256), WgCfg<2>::LDS, s, a);
+  else if (aligned)
+    hipLaunchKernelGGL(wgrad2_kernel<1>, dim3((unsigned)nblk), dim3(256), WgCfg<1>::LDS, s, a);
+  else if (upsample == 2)
     hipLaunchKernelGGL(wgrad_kernel<2>, dim3((unsigned)nblk), dim3(256), WgCfg<2>::LDS, s, a);
   else
     hipLaunchKernelGGL(wgrad_kernel<1>, dim3((unsigned)nblk), dim3(256), WgCfg<1>::LDS, s, a);

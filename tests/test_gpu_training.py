@@ -91,6 +91,10 @@ DEC_CASES = [
     (1, 64, 16, 32, 3, 1, False),   # final decoder conv
     (1, 4, 2, 2, 64, 1, True),      # smallest reflect-padded map
     (1, 12, 1, 3, 64, 2, True),     # upsampled 1-row map
+    # aligned shapes (Cin, Cout % 64 == 0, W % 32 == 0): the prefetching wgrad2 kernel
+    (2, 64, 6, 32, 64, 1, True),
+    (1, 128, 4, 16, 64, 2, True),
+    (1, 64, 2, 64, 128, 1, False),
 ]
 
 
