@@ -68,6 +68,13 @@ SIGNATURES = {
     "ast_soft_hist_backward_f32": (_i, [_p, _i, _ll, _f, _p, _p, _i, _p]),
     "ast_range_loss_f32": (_i, [_p, _ll, _f, _p, _p, _p, _i, _p]),
     "ast_sqdiff_mean_f32": (_i, [_p, _p, _ll, _f, _p, _p, _p, _i, _p]),
+    "ast_aug_to_tensor": (_i, [_p, _i, _i, _i, _p, _p]),
+    "ast_aug_remap_f32": (_i, [_p, _i, _i, _i, _p, _i, _i, _p, _p]),
+    "ast_aug_gray_sum_f32": (_i, [_p, _i, _i, _p, _p]),
+    "ast_aug_color_f32": (_i, [_p, _i, _i, _i, _f, _p, _p, _p]),
+    "ast_aug_resize_workspace_floats": (ctypes.c_size_t, [_i, _i, _i]),
+    "ast_aug_resize_f32": (_i, [_p, _i, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _p]),
+    "ast_aug_blur_f32": (_i, [_p, _i, _i, _i, _p, _i, _p, _p, _p]),
 }
 
 ERRORS = {-1: "null pointer", -2: "bad shape", -3: "unsupported configuration"}

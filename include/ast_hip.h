@@ -328,6 +328,40 @@ int ast_range_loss_f32(const float* x, long long numel, float weight, const floa
 int ast_sqdiff_mean_f32(const float* x, const float* y, long long numel, float weight,
                         const float* gscale, float* loss, float* dx, int accumulate, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * On-device augmentation (SURVEY §8f "next" #3): the get_transform pipeline of data_loader.py:110-135
+ * on [C][H][W] fp32 images (torchvision tensor semantics). Random parameters are drawn by the caller.
+ * ------------------------------------------------------------------------------------------ */
+
+/* transforms.ToTensor: uint8 [h][w][cs] (cs >= 3; RGB first) -> fp32 [3][h][w] / 255. */
+int ast_aug_to_tensor(const unsigned char* src, int h, int w, int cs, float* dst, void* stream);
+
+/* Integer-affine gather (torch.rot90 / hflip / vflip, data_loader.py:14-24, :115-116):
+ * dst[c][y][x] = src[c][sy][sx], sy = coef[0]*y + coef[1]*x + coef[2], sx = coef[3]*y + coef[4]*x +
+ * coef[5]; coef is a HOST array of 6 ints; every (y, x) must map inside src. */
+int ast_aug_remap_f32(const float* src, int c, int hi, int wi, float* dst, int ho, int wo,
+                      const int* coef, void* stream);
+
+/* *acc = sum over pixels of rgb_to_grayscale(img) (zeroed here; adjust_contrast's mean * h*w). */
+int ast_aug_gray_sum_f32(const float* img, int h, int w, float* acc, void* stream);
+
+/* ColorJitter's adjustments and RandomGrayscale on a 3-channel image: op 0 brightness, 1 contrast
+ * (gray_sum from ast_aug_gray_sum_f32), 2 saturation, 3 hue (factor in [-0.5, 0.5]), 4 grayscale. */
+int ast_aug_color_f32(const float* src, int h, int w, int op, float factor, const float* gray_sum,
+                      float* dst, void* stream);
+
+/* Resize / RandomResizedCrop: the crop [y0, y0+crop_h) x [x0, x0+crop_w) of src resized to ho x wo
+ * with antialiased bilinear weights (torch upsample aa, align_corners=False). tmp: device scratch
+ * of ast_aug_resize_workspace_floats(c, crop_h, wo) floats. */
+size_t ast_aug_resize_workspace_floats(int c, int crop_h, int wo);
+int ast_aug_resize_f32(const float* src, int c, int h, int w, int y0, int x0, int crop_h, int crop_w,
+                       float* dst, int ho, int wo, float* tmp, void* stream);
+
+/* GaussianBlur: separable normalised taps (HOST array of k floats, k odd <= 15), reflect padding;
+ * tmp: device scratch of c*h*w floats. */
+int ast_aug_blur_f32(const float* src, int c, int h, int w, const float* taps, int k, float* dst,
+                     float* tmp, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

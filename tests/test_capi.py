@@ -85,3 +85,12 @@ def test_cpu_tensors_are_rejected():
         ops.adain(torch.zeros(1, 2, 3, 3), torch.zeros(1, 2, 3, 3))
     with pytest.raises(_lib.HipOpError):
         ops.pack_conv3x3(torch.zeros(4, 3, 3, 3))
+
+
+def test_data_loader_module_mirrors_reference_names():
+    """The drop-in data_loader exposes the reference's public names (data_loader.py)."""
+    from arbitrarystyletransfer_amd import data_loader as DL
+    for name in ("Random90Rot", "ConditionalResize", "RandomResizeOrCrop", "RandomBlur", "ImageTransform",
+                 "get_transform", "image_loader", "infinite_sampler", "InfiniteSamplerWrapper",
+                 "FlatFolderDataset", "FlatFolderDatasetAE"):
+        assert hasattr(DL, name), name
