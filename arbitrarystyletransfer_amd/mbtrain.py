@@ -1,0 +1,297 @@
+"""Training path of the MobileNet-variant modules (SURVEY.md §8f "next" #4: AutoEncoder training,
+train_autoencoder.py:88-148) on the HIP kernels of csrc/mbtrain.hip.
+
+The inference path (mobilenetv2.DepthWiseConv.run) folds eval-mode BatchNorm into the weights and
+fuses whole blocks; training needs batch statistics and every intermediate, so here each layer of
+a block's `_layers` (mobilenetv2.py:95-165, same order) is an autograd Function whose forward and
+backward are HIP launches: 1x1 convs as MFMA GEMMs, depthwise convs, BatchNorm2d (training mode,
+running statistics updated as torch does), Hardswish, SELayer, the residual add and the decoder's
+nearest upsample. fp32 only (the reference trains in fp32).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._lib import HipOpError, check, lib, ptr, stream_ptr
+
+
+def _s(t):
+    return stream_ptr(t.device)
+
+
+def _f32(t, name):
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise HipOpError(f"{name} must be a tensor on a HIP device")
+    if t.dtype != torch.float32:
+        raise HipOpError(f"{name}: the training path runs in float32, got {t.dtype}")
+    return t.contiguous()
+
+
+def gemm(A, B, C, M, N, K, batch, sA, sB, sC, ksplit=1, accumulate=False):
+    """C[b][m][n] (+)= sum_k A[b][m][k] B[b][k][n]; sA/sB/sC = (batch, row, col) element strides."""
+    check(ops._timed("mbgemm", 2 * M * N * K * batch, C.device, lambda: lib().ast_mbt_gemm_f32(
+        ptr(A), ptr(B), ptr(C), M, N, K, batch, *sA, *sB, *sC, ksplit, int(accumulate), 0, _s(C))), "gemm")
+
+
+def _ksplit(p):
+    return max(1, min(64, p // 4096))
+
+
+# ------------------------------------------------------------------------------------------------
+# 1x1 conv (no bias), optionally over a channel-split input (the un-materialised torch.cat)
+# ------------------------------------------------------------------------------------------------
+class PwConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, x2, weight):
+        x = _f32(x, "x")
+        n, c1, h, w = x.shape
+        P = h * w
+        cout, cin = weight.shape[0], weight.shape[1]
+        wt = weight.detach().reshape(cout, cin).contiguous()
+        y = torch.empty((n, cout, h, w), device=x.device, dtype=torch.float32)
+        gemm(wt, x, y, cout, P, c1, n, (0, cin, 1), (c1 * P, P, 1), (cout * P, P, 1))
+        if x2 is not None:
+            x2 = _f32(x2, "x2")
+            c2 = x2.shape[1]
+            gemm(wt[:, c1:], x2, y, cout, P, c2, n, (0, cin, 1), (c2 * P, P, 1), (cout * P, P, 1), accumulate=True)
+        ctx.save_for_backward(x, x2 if x2 is not None else x, wt)
+        ctx.has_x2 = x2 is not None
+        ctx.wshape = weight.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, x2, wt = ctx.saved_tensors
+        g = _f32(g, "grad")
+        n, cout, h, w = g.shape
+        P = h * w
+        cin = wt.shape[1]
+        c1 = x.shape[1]
+        dx = dx2 = dw = None
+        parts = [(x, 0)] + ([(x2, c1)] if ctx.has_x2 else [])
+        grads = []
+        for xi, off in parts:
+            ci = xi.shape[1]
+            d = None
+            if ctx.needs_input_grad[0 if off == 0 else 1]:
+                d = torch.empty_like(xi)
+                gemm(wt[:, off:], g, d, ci, P, cout, n, (0, 1, cin), (cout * P, P, 1), (ci * P, P, 1))
+            grads.append(d)
+        dx = grads[0]
+        if ctx.has_x2:
+            dx2 = grads[1]
+        if ctx.needs_input_grad[2]:
+            dw = torch.zeros((cout, cin), device=g.device, dtype=torch.float32)
+            for xi, off in parts:
+                ci = xi.shape[1]
+                gemm(g, xi, dw[:, off:], cout, ci, P, n, (cout * P, P, 1), (ci * P, 1, P), (0, cin, 1),
+                     ksplit=_ksplit(P))
+            dw = dw.reshape(ctx.wshape)
+        return dx, dx2, dw
+
+
+class DwConvFn(torch.autograd.Function):
+    """Depthwise k x k conv, stride s, reflect padding (k-1)/2."""
+
+    @staticmethod
+    def forward(ctx, x, weight, k, s):
+        x = _f32(x, "x")
+        n, c, h, w = x.shape
+        p = (k - 1) // 2
+        ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+        wt = weight.detach().reshape(c, k * k).contiguous()
+        y = torch.empty((n, c, ho, wo), device=x.device, dtype=torch.float32)
+        check(lib().ast_mbt_dw_f32(0, ptr(x), ptr(wt), None, ptr(y), n, c, h, w, k, s, _s(x)), "dw conv")
+        ctx.save_for_backward(x, wt)
+        ctx.k, ctx.s, ctx.wshape = k, s, weight.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, wt = ctx.saved_tensors
+        g = _f32(g, "grad")
+        n, c, h, w = x.shape
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            check(lib().ast_mbt_dw_f32(1, None, ptr(wt), ptr(g), ptr(dx), n, c, h, w, ctx.k, ctx.s, _s(g)), "dw dgrad")
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty((c, ctx.k * ctx.k), device=g.device, dtype=torch.float32)
+            check(lib().ast_mbt_dw_f32(2, ptr(x), ptr(wt), ptr(g), ptr(dw), n, c, h, w, ctx.k, ctx.s, _s(g)),
+                  "dw wgrad")
+            dw = dw.reshape(ctx.wshape)
+        return dx, dw, None, None
+
+
+class BatchNormTrainFn(torch.autograd.Function):
+    """BatchNorm2d.forward in training mode (batch statistics; running stats updated in place)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bn):
+        x = _f32(x, "x")
+        n, c, h, w = x.shape
+        mean = torch.empty((c,), device=x.device, dtype=torch.float32)
+        invstd = torch.empty_like(mean)
+        y = torch.empty_like(x)
+        track = bn.track_running_stats and bn.running_mean is not None
+        momentum = bn.momentum if bn.momentum is not None else 0.1
+        check(lib().ast_mbt_bn_fwd_f32(ptr(x), n, c, h * w, ptr(gamma), ptr(beta), float(bn.eps), float(momentum),
+                                       ptr(mean), ptr(invstd), ptr(bn.running_mean) if track else None,
+                                       ptr(bn.running_var) if track else None, ptr(y), _s(x)), "batch norm")
+        if track:
+            bn.num_batches_tracked.add_(1)   # bookkeeping counter (torch does the same host-side increment)
+        ctx.save_for_backward(x, gamma, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, gamma, mean, invstd = ctx.saved_tensors
+        g = _f32(g, "grad")
+        n, c, h, w = x.shape
+        dx = torch.empty_like(x)
+        dgamma = torch.empty_like(mean)
+        dbeta = torch.empty_like(mean)
+        check(lib().ast_mbt_bn_bwd_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma), ptr(dgamma),
+                                       ptr(dbeta), ptr(dx), _s(g)), "batch norm backward")
+        return dx, dgamma, dbeta, None
+
+
+class HardswishFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = _f32(x, "x")
+        y = torch.empty_like(x)
+        check(lib().ast_mbt_eltwise_f32(0, ptr(x), None, ptr(y), x.numel(), 0, 0, _s(x)), "hardswish")
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        check(lib().ast_mbt_eltwise_f32(1, ptr(x), ptr(_f32(g, "grad")), ptr(dx), x.numel(), 0, 0, _s(x)),
+              "hardswish backward")
+        return dx
+
+
+class AddFn(torch.autograd.Function):
+    """The residual `x + org_x` (mobilenetv2.py:162-163)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = _f32(a, "a"), _f32(b, "b")
+        y = torch.empty_like(a)
+        check(lib().ast_mbt_eltwise_f32(2, ptr(a), ptr(b), ptr(y), a.numel(), 0, 0, _s(a)), "add")
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+class Upsample2Fn(torch.autograd.Function):
+    """nn.Upsample(scale_factor=2, mode="nearest") (models.py:266)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = _f32(x, "x")
+        n, c, h, w = x.shape
+        y = torch.empty((n, c, 2 * h, 2 * w), device=x.device, dtype=torch.float32)
+        check(lib().ast_mbt_eltwise_f32(3, ptr(x), None, ptr(y), n * c, h, w, _s(x)), "upsample")
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        n, c, h, w = ctx.shape
+        dx = torch.empty(ctx.shape, device=g.device, dtype=torch.float32)
+        check(lib().ast_mbt_eltwise_f32(4, ptr(_f32(g, "grad")), None, ptr(dx), n * c, h, w, _s(g)), "upsample bwd")
+        return dx
+
+
+class SEFn(torch.autograd.Function):
+    """SELayer.forward (mobilenetv2.py:72-81): x * Hardtanh(0,1)(fc2(relu(fc1(avgpool(x)))))."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        x = _f32(x, "x")
+        n, c, h, w = x.shape
+        red = w1.shape[0]
+        pool = torch.empty((n, c), device=x.device, dtype=torch.float32)
+        check(lib().ast_mbt_plane_f32(0, ptr(x), None, None, None, ptr(pool), n * c, h * w, _s(x)), "se pool")
+        hid = torch.empty((n, red), device=x.device, dtype=torch.float32)
+        z = torch.empty((n, c), device=x.device, dtype=torch.float32)
+        gate = torch.empty_like(z)
+        w1c, w2c = w1.detach().contiguous(), w2.detach().contiguous()
+        check(lib().ast_mbt_se_fc_fwd_f32(ptr(pool), ptr(w1c), ptr(b1), ptr(w2c), ptr(b2), n, c, red, ptr(hid), ptr(z),
+                                          ptr(gate), _s(x)), "se fc")
+        y = torch.empty_like(x)
+        check(lib().ast_mbt_plane_f32(2, ptr(x), None, ptr(gate), None, ptr(y), n * c, h * w, _s(x)), "se scale")
+        ctx.save_for_backward(x, w1c, w2c, pool, hid, z, gate)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w1, w2, pool, hid, z, gate = ctx.saved_tensors
+        g = _f32(g, "grad")
+        n, c, h, w = x.shape
+        red = w1.shape[0]
+        dgate = torch.empty((n, c), device=x.device, dtype=torch.float32)
+        check(lib().ast_mbt_plane_f32(1, ptr(g), ptr(x), None, None, ptr(dgate), n * c, h * w, _s(g)), "se dgate")
+        dw1, db1 = torch.empty_like(w1), torch.empty((red,), device=x.device, dtype=torch.float32)
+        dw2, db2 = torch.empty_like(w2), torch.empty((c,), device=x.device, dtype=torch.float32)
+        dpool = torch.empty((n, c), device=x.device, dtype=torch.float32)
+        check(lib().ast_mbt_se_fc_bwd_f32(ptr(dgate), ptr(z), ptr(hid), ptr(pool), ptr(w1), ptr(w2), n, c, red, h * w,
+                                          ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), ptr(dpool), _s(g)), "se fc bwd")
+        dx = torch.empty_like(x)
+        check(lib().ast_mbt_plane_f32(2, ptr(g), None, ptr(gate), ptr(dpool), ptr(dx), n * c, h * w, _s(g)),
+              "se dx")
+        return dx, dw1, db1, dw2, db2
+
+
+def block_forward(block, x, x2=None, up: int = 1):
+    """DepthWiseConv.forward (mobilenetv2.py:153-165) layer by layer, BatchNorm in the module's
+    mode (training: batch statistics). `up` applies DecoderBlock's nearest upsample first."""
+    if x.dtype != torch.float32:
+        raise HipOpError("the MobileNet training path runs in float32")
+    if up == 2:
+        x = Upsample2Fn.apply(x)
+    org_x = x
+    h = x
+    first_conv = True
+    for layer in block._layers:
+        if isinstance(layer, nn.ReflectionPad2d):
+            continue  # the ratio-1 block's pad: the depthwise kernel pads reflect by (k-1)/2 = 1
+        if isinstance(layer, nn.Conv2d):
+            if layer.groups > 1:
+                k = layer.kernel_size[0]
+                h = DwConvFn.apply(h, layer.weight, k, layer.stride[0])
+            else:
+                h = PwConvFn.apply(h, x2 if first_conv else None, layer.weight)
+            first_conv = False
+        elif isinstance(layer, nn.BatchNorm2d):
+            if layer.training:
+                h = BatchNormTrainFn.apply(h, layer.weight, layer.bias, layer)
+            else:
+                raise NotImplementedError("eval-mode BatchNorm under autograd: use the inference path "
+                                          "(torch.no_grad()) or train mode")
+        elif isinstance(layer, nn.Hardswish):
+            h = HardswishFn.apply(h)
+        elif layer.__class__.__name__ == "SELayer":
+            fc1, fc2 = layer.fc[0], layer.fc[2]
+            h = SEFn.apply(h, fc1.weight, fc1.bias, fc2.weight, fc2.bias)
+        else:
+            raise NotImplementedError(f"layer {layer.__class__.__name__} in the training path")
+    if block.identity:
+        h = AddFn.apply(h, org_x)
+    return h
+
+
+def wants_training_path(module, *xs) -> bool:
+    """True when a forward must record autograd through the HIP training kernels."""
+    if not torch.is_grad_enabled():
+        return False
+    return any(p.requires_grad for p in module.parameters()) or any(
+        x is not None and x.requires_grad for x in xs)

@@ -20,7 +20,7 @@ import math
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import mbtrain, ops
 from ._lib import HipOpError, check, lib, ptr, stream_ptr
 
 __all__ = ["_make_divisible", "conv_3x3_bn", "SELayer", "DepthWiseConv"]
@@ -87,6 +87,11 @@ class _Conv3x3HS(nn.Sequential):
 
     def forward(self, x):
         conv = self[0]
+        if mbtrain.wants_training_path(self, x):
+            from . import functional as Fn
+            y = Fn.DecoderConvFn.apply(x.float().contiguous(), conv.weight, None,
+                                       ops.pack_conv3x3(conv.weight.detach().float()), 1, False)
+            return mbtrain.HardswishFn.apply(y)
         check_inference(x, self)
         dt = act_dtype(self)
         if not isinstance(x, torch.Tensor) or x.device.type != "cuda" or x.dim() != 4:
@@ -246,6 +251,8 @@ class DepthWiseConv(nn.Module):
 
     def run(self, x, x2=None, up: int = 1):
         """Block forward on x (or cat(x, x2) along channels), after a nearest x`up` upsample."""
+        if mbtrain.wants_training_path(self, x, x2) or (self.use_norm and self.training):
+            return mbtrain.block_forward(self, x, x2, up)   # layer by layer, with backward
         if self.use_norm and self.training:
             raise NotImplementedError("DepthWiseConv with BatchNorm in training mode (batch statistics) is not "
                                       "implemented on the HIP path; call .eval() (running statistics)")

@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F  # noqa: F401  (re-exported like the reference)
 
 from . import functional as Fn
-from . import ops, synth
+from . import mbtrain, ops, synth
 from .conf import *  # noqa: F401,F403
 from .conf import device  # noqa: F401
 from .losses import *  # noqa: F401,F403
@@ -370,6 +370,8 @@ class Encoder(nn.Module):
             return x
         outs = []
         last = max(out_layers) if len(out_layers) else -1   # later blocks cannot change the result
+        if self.training and mbtrain.wants_training_path(self, x):
+            last = len(self.mob_net) - 1   # train mode: every block runs (BatchNorm running statistics)
         for i, layer in enumerate(self.mob_net):
             if i > last:
                 break
@@ -397,7 +399,7 @@ class DecoderBlock(nn.Module):
     def forward(self, x):
         x = self._conv(x)
         if self._should_upsample:
-            x = self._upsample_2.run(x, None, up=2)
+            x = self._upsample_2.run(x, None, up=2)   # training path: explicit upsample, then the block
         return x
 
 
@@ -426,6 +428,12 @@ class Decoder(nn.Module):
 
     def _image_conv(self, x):
         conv = self._img_out
+        if mbtrain.wants_training_path(self, x):
+            y = Fn.DecoderConvFn.apply(x.float().contiguous(), conv.weight, conv.bias,
+                                       ops.pack_conv3x3(conv.weight.detach().float()), 1, False)
+            if self.exporting:
+                raise NotImplementedError("Hardtanh output under autograd (exporting=True) is inference-only")
+            return y
         check_inference(x, self)
         dt = act_dtype(self)
         if x.dtype != dt or x.device.type != "cuda" or x.dim() != 4 or x.shape[1] != conv.in_channels:

@@ -145,3 +145,88 @@ class AdaINTrainer:
         self.optim.load_state_dict(d["ast_optim"])
         with open(self.train_dict_file) as f:
             self.train_dict = json.load(f)
+
+
+# ------------------------------------------------------------------------------------------------
+# AutoEncoder training (train_autoencoder.py:16-148; SURVEY.md §8f "next" #4)
+# ------------------------------------------------------------------------------------------------
+
+def default_ae_args(**kw):
+    """train_autoencoder.py:250-264 defaults."""
+    a = dict(train_iter=8192, batch_size=16, lr=2e-4, save_dir="models/auto_encoder/", load=False,
+             recon_lam=100.0, perp_lam=0.01)
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+class AutoencoderTrainer:
+    """AutoencoderTrainer (train_autoencoder.py:16-148) on HIP: the MobileNet AutoEncoder in
+    training mode (BatchNorm batch statistics, mbtrain.py), reconstruction Huber loss plus the
+    perceptual Huber loss over the frozen VGG loss network's six layers, clip_grad_norm_(10) and
+    Adam(betas (0.9, 0.99), eps 1e-7), fused (optim.FusedAdam). Checkpoint and train_dict.json
+    layout as the reference (ae.pth {"AE", "optim"}; train_loss / val_loss / perp_loss)."""
+
+    def __init__(self, args=None, content_iter=None, val_loader=None, device=None, model=None, lossnet=None):
+        self.args = args or default_ae_args()
+        self.device = torch.device(device or "cuda")
+        self.content_iter, self.val_loader = content_iter, val_loader
+        self.model = (model or models.AutoEncoder()).to(self.device).train()
+        self.pretrained_mobnet = (lossnet or models.PretrainedEncoder()).to(self.device).eval()
+        self.pretrained_mobnet.requires_grad_(False)
+        self.ae_optim = FusedAdam(list(self.model.parameters()), lr=self.args.lr, betas=(0.9, 0.99), eps=1e-7,
+                                  max_grad_norm=10.0)
+        self.save_file = os.path.join(self.args.save_dir, "ae.pth")
+        self.train_dict_file = os.path.join(self.args.save_dir, "train_dict.json")
+        self.train_dict = {"train_loss": [], "val_loss": [], "perp_loss": []}
+
+    def compute_losses(self, content_imgs):
+        recon_imgs = self.model(content_imgs)
+        recon_loss = L.compute_content_loss(recon_imgs, content_imgs)                  # nn.HuberLoss(), :129
+        with torch.no_grad():
+            content_maps = self.pretrained_mobnet(content_imgs)                        # :132
+        recon_maps = self.pretrained_mobnet(recon_imgs)                                # :133
+        terms = [L.compute_content_loss(r, c) for r, c in zip(recon_maps, content_maps)]   # :137-151
+        content_loss = torch.stack(terms).sum()
+        loss = self.args.recon_lam * recon_loss + self.args.perp_lam * content_loss   # :156
+        return {"loss": loss, "recon_loss": recon_loss, "content_loss": content_loss, "recon": recon_imgs}
+
+    def train_step(self, content_imgs, record=True):
+        out = self.compute_losses(content_imgs)
+        self.ae_optim.zero_grad(set_to_none=True)
+        out["loss"].backward()
+        self.ae_optim.step()                                                           # clip 10 + Adam, :159-165
+        out["grad_norm"] = self.ae_optim.last_grad_norm
+        if record:
+            self.train_dict["train_loss"].append(float(out["recon_loss"].item()))
+            self.train_dict["perp_loss"].append(float(out["content_loss"].item()))
+        return out
+
+    def train(self):
+        for cur_iter in range(self.args.train_iter):
+            if (cur_iter + 1) % 32 == 0:
+                self.save()
+                if (cur_iter + 1) % 64 == 0 and self.val_loader is not None:
+                    self.validate()
+            self.train_step(next(self.content_iter).to(self.device))
+
+    @torch.no_grad()
+    def validate(self):
+        """train_autoencoder.py:71-82 (mean absolute reconstruction error per image; a logged metric)."""
+        val_imgs = next(self.val_loader).to(self.device)
+        self.model.eval()
+        recon_imgs = self.model(val_imgs)
+        self.train_dict["val_loss"].append(float((val_imgs - recon_imgs).abs().mean().item()) / val_imgs.shape[0])
+        self.model.train()
+
+    def save(self):
+        os.makedirs(self.args.save_dir, exist_ok=True)
+        torch.save({"AE": self.model.state_dict(), "optim": self.ae_optim.state_dict()}, self.save_file)
+        with open(self.train_dict_file, "w") as f:
+            json.dump(self.train_dict, f)
+
+    def load(self):
+        d = torch.load(self.save_file, map_location=self.device, weights_only=True)
+        self.model.load_state_dict(d["AE"])
+        self.ae_optim.load_state_dict(d["optim"])
+        with open(self.train_dict_file) as f:
+            self.train_dict = json.load(f)

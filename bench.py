@@ -46,9 +46,9 @@ def parse():
     p.add_argument("--size", type=int, default=None, help="image side (config 2: 512, config 5: 1024)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(os.cpu_count(), OMP_NUM_THREADS or 16)")
-    p.add_argument("--mode", choices=["fwd", "train", "mobilenet"], default="fwd",
+    p.add_argument("--mode", choices=["fwd", "train", "mobilenet", "ae-train"], default="fwd",
                    help="fwd: config 2 (the headline metric); train: config 3/4 AdaIN training step; "
-                        "mobilenet: config 5")
+                        "mobilenet: config 5; ae-train: train_autoencoder.py step (SURVEY §8f next #4)")
     p.add_argument("--full-losses", action="store_true",
                    help="train mode: add train.py's hist, org_img and out_of_range terms (SURVEY §8f next #2)")
     p.add_argument("--attention", action="store_true",
@@ -111,6 +111,63 @@ def train_bench(args, dev, rank, world):
                      "traffic": None, "wgrad_tflops": wg_tf,
                      "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3),
                      "mfma_tflop_per_step": fl / args.steps / 1e12},
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def ae_train_bench(args, dev, rank, world):
+    """AutoEncoder training step (train_autoencoder.py:124-165): the MobileNet
+    AutoEncoder in training mode (BatchNorm batch statistics), reconstruction + perceptual Huber
+    losses through the frozen VGG loss network, backward, clip 10 + Adam. bs=16 at 160x160 (the
+    reference's batch size and its largest training size, conf.py img_sizes). N > 1: each rank
+    steps its own replica on its own batch (replicas only; the reference trains on one GPU)."""
+    from arbitrarystyletransfer_amd.train import AutoencoderTrainer, default_ae_args
+    B, S = args.batch or 16, args.size or 160
+    trainer = AutoencoderTrainer(default_ae_args(batch_size=B), device=dev,
+                                 model=models.AutoEncoder().load_live_init())
+    content = torch.from_numpy(synth.image(901 + rank, (B, 3, S, S))).to(dev)
+    for _ in range(args.warmup):
+        trainer.train_step(content, record=False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    timer = ops.LaunchTimer()
+    t0 = time.perf_counter()
+    with timer:
+        for _ in range(args.steps):
+            out = trainer.train_step(content, record=False)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out["loss"]), "non-finite loss"
+    fam = {}
+    for tag, fl, ms in timer.results():
+        k = tag.split()[0]
+        f0, m0, c0 = fam.get(k, (0.0, 0.0, 0))
+        fam[k] = (f0 + fl, m0 + ms, c0 + 1)
+    mm = [fam[k] for k in fam if k.startswith(("conv3x3", "wgrad"))]
+    fl, ms = sum(f for f, _, _ in mm), sum(m for _, m, _ in mm)
+    tf = fl / (ms * 1e-3) / 1e12 if ms else 0.0
+    result = {
+        "metric": "AutoEncoder training images/sec (train_autoencoder.py step)",
+        "value": B * world * args.steps / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (live-init weights, U[0,1) images), resident in HBM",
+        "config": {"workload": f"AutoEncoder train step (MobileNet encoder/decoder, BatchNorm train mode; recon + "
+                               f"perceptual Huber via VGG relu_1..relu_15; clip 10 + Adam), bs={B}/GPU {S}x{S} fp32",
+                   "global_batch": B * world, "image_size": S, "parallelism": f"replicas x{world}"},
+        "roofline": {"bound": "mfma", "kernel": "conv3x3 fwd/dgrad + wgrad MFMA launches of a step",
+                     "achieved": tf, "peak": PEAK_FP32_MFMA_TF, "unit": "TFLOP/s", "frac": tf / PEAK_FP32_MFMA_TF,
+                     "traffic": None, "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3)},
+        "kernels_ms_per_step": {k: round(m / args.steps, 4) for k, (f, m, c) in sorted(fam.items())},
+        "mbgemm_tflops": (fam["mbgemm"][0] / (fam["mbgemm"][1] * 1e-3) / 1e12) if "mbgemm" in fam else None,
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -287,8 +344,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    if args.mode in ("train", "mobilenet"):
-        (train_bench if args.mode == "train" else mobilenet_bench)(args, dev, rank, world)
+    if args.mode in ("train", "mobilenet", "ae-train"):
+        {"train": train_bench, "mobilenet": mobilenet_bench, "ae-train": ae_train_bench}[args.mode](args, dev, rank, world)
         if world > 1:
             dist.destroy_process_group()
         return

@@ -362,6 +362,52 @@ int ast_aug_resize_f32(const float* src, int c, int h, int w, int y0, int x0, in
 int ast_aug_blur_f32(const float* src, int c, int h, int w, const float* taps, int k, float* dst,
                      float* tmp, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * MobileNet-variant training (SURVEY §8f "next" #4: AutoEncoder training, train_autoencoder.py),
+ * fp32, composable kernels with their backward (csrc/mbtrain.hip).
+ * ------------------------------------------------------------------------------------------ */
+
+/* C[b][m][n] (+)= sum_k A[b][m][k] B[b][k][n] with element strides (1x1 convs and their grads).
+ * ksplit > 1 splits K across workgroups; partial sums are then atomically added (as when C is
+ * shared across the batch, sCb == 0): C must hold the starting value (zero it to overwrite). */
+int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int K, int batch,
+                     long long sAb, long long sAm, long long sAk, long long sBb, long long sBk,
+                     long long sBn, long long sCb, long long sCm, long long sCn, int ksplit,
+                     int accumulate, int atomic, void* stream);
+
+/* Depthwise k x k conv (k 3|5, stride 1|2, reflect pad (k-1)/2; mobilenetv2.py:148-149, :116-117):
+ * mode 0 out = conv(x, w); 1 out = dx from g (overwritten); 2 out = dw [c][k*k] from x, g. */
+int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, float* out, int n,
+                   int c, int h, int wd, int k, int s, void* stream);
+
+/* BatchNorm2d in training mode (batch statistics, biased var + eps; running stats updated with
+ * momentum and the unbiased variance when run_mean/run_var are given). mean/invstd [c] saved. */
+int ast_mbt_bn_fwd_f32(const float* x, int n, int c, long long hw, const float* gamma,
+                       const float* beta, float eps, float momentum, float* mean, float* invstd,
+                       float* run_mean, float* run_var, float* y, void* stream);
+int ast_mbt_bn_bwd_f32(const float* x, const float* dy, int n, int c, long long hw,
+                       const float* mean, const float* invstd, const float* gamma, float* dgamma,
+                       float* dbeta, float* dx, void* stream);
+
+/* op 0 y = hardswish(a); 1 y = hardswish'(a) * b; 2 y = a + b; 3 y = nearest-upsample x2 of a
+ * (n planes of h x w); 4 its backward (a = grad of the 2h x 2w planes). */
+int ast_mbt_eltwise_f32(int op, const float* a, const float* b, float* y, long long n, int h,
+                        int w, void* stream);
+
+/* op 0 out[p] = mean(x[p]) (AdaptiveAvgPool2d(1)); 1 out[p] = sum(x[p] * y[p]);
+ * 2 out = x * gate[p] (+ gadd[p]) over planes of hw elements. */
+int ast_mbt_plane_f32(int op, const float* x, const float* y, const float* gate, const float* gadd,
+                      float* out, long long planes, long long hw, void* stream);
+
+/* SELayer MLP (mobilenetv2.py:63-81): hid = relu(W1 pool + b1), z = W2 hid + b2, gate = clamp(z,0,1);
+ * backward from dgate: parameter gradients (overwritten) and dpool / hw. */
+int ast_mbt_se_fc_fwd_f32(const float* pool, const float* w1, const float* b1, const float* w2,
+                          const float* b2, int n, int c, int red, float* hid, float* z, float* gate,
+                          void* stream);
+int ast_mbt_se_fc_bwd_f32(const float* dgate, const float* z, const float* hid, const float* pool,
+                          const float* w1, const float* w2, int n, int c, int red, long long hw,
+                          float* dw1, float* db1, float* dw2, float* db2, float* dpool, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -192,6 +192,7 @@ def main():
     hist_golden(R)
     train_step_golden(R, enc_wb, dec_wb)
     train_step_golden(R, enc_wb, dec_wb, full=True)
+    ae_train_golden(R)
     mobilenet_golden(R)
     adaattn_golden(R)
     print("golden vectors written to", HERE)
@@ -320,6 +321,54 @@ def hist_golden(R):
                         range_loss=r.detach().numpy(), range_grad=x.grad.numpy())
 
 
+def ae_train_golden(R):
+    """One AutoEncoder training step (train_autoencoder.py:124-165) from the reference's own
+    modules and losses: AutoEncoder (live init 5/6/7) in train mode (BatchNorm batch statistics),
+    HuberLoss reconstruction + perceptual Huber over PretrainedEncoder's six layers (VGG live init
+    1), clip_grad_norm_(10), Adam(lr 2e-4, betas (0.9, 0.99), eps 1e-7)."""
+    L = R["_losses"]
+    torch.manual_seed(0)
+    ae = R["AutoEncoder"]()
+    synth.live_init_(ae.encoder, 5)
+    synth.live_init_(ae.decoder, 6)
+    synth.live_init_(ae.ada_out, 7)
+    ae.train()
+    lossnet = R["PretrainedEncoder"]().eval()
+    set_convs(lossnet, synth.vgg_encoder_weights(1))
+    for p in lossnet.parameters():
+        p.requires_grad_(False)
+    params = list(ae.parameters())
+    opt = torch.optim.Adam(params, lr=2e-4, betas=[0.9, 0.99], eps=1e-7)
+    content = torch.from_numpy(synth.image(971, (2, 3, 64, 64)))
+    recon = ae(content)
+    recon_loss = torch.nn.HuberLoss()(recon, content)
+    content_maps = lossnet(content)
+    recon_maps = lossnet(recon)
+    for i in range(len(content_maps)):
+        term = L.compute_content_loss(recon_maps[i], content_maps[i].detach())
+        content_loss = term if i == 0 else content_loss + term
+    loss = 100.0 * recon_loss + 0.01 * content_loss
+    opt.zero_grad()
+    loss.backward()
+    names = [n for n, _ in ae.named_parameters()]
+    grads = {n: (p.grad.detach().clone() if p.grad is not None else None) for n, p in zip(names, params)}
+    norm = torch.nn.utils.clip_grad_norm_(params, 10.0)
+    opt.step()
+    out = dict(content=content.numpy(), recon=recon.detach().numpy(), recon_loss=recon_loss.detach().numpy(),
+               content_loss=content_loss.detach().numpy(), loss=loss.detach().numpy(), grad_norm=norm.detach().numpy())
+    for n, p in zip(names, params):
+        g = grads[n]
+        if g is None:
+            out[f"nograd:{n}"] = np.array(1)
+            continue
+        out[f"grad:{n}"] = g.numpy() if g.numel() <= 2048 else g.reshape(-1)[::17].numpy()
+        out[f"param:{n}"] = p.detach().numpy() if p.numel() <= 2048 else p.detach().reshape(-1)[::17].numpy()
+    for n, b in ae.named_buffers():
+        if "running" in n:
+            out[f"buf:{n}"] = b.numpy()
+    np.savez_compressed(os.path.join(HERE, "ae_train_step_64.npz"), **out)
+
+
 def train_step_golden(R, enc_wb, dec_wb, full=False):
     """One AdaIN training step assembled from the reference's own functions
     exactly as train.py:191-300 assembles its losses: lifted PretrainedEncoder / AdaIN /
@@ -399,6 +448,8 @@ if __name__ == "__main__":
         adaattn_golden(load_reference())
     elif "--hist" in sys.argv:
         hist_golden(load_reference())
+    elif "--ae-train" in sys.argv:
+        ae_train_golden(load_reference())
     elif "--train-full" in sys.argv:
         train_step_golden(load_reference(), synth.vgg_encoder_weights(1), synth.vgg_decoder_weights(2), full=True)
     else:
