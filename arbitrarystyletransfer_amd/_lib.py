@@ -75,10 +75,12 @@ SIGNATURES = {
     "ast_aug_resize_workspace_floats": (ctypes.c_size_t, [_i, _i, _i]),
     "ast_aug_resize_f32": (_i, [_p, _i, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _p]),
     "ast_aug_blur_f32": (_i, [_p, _i, _i, _i, _p, _i, _p, _p, _p]),
-    "ast_mbt_gemm_f32": (_i, [_p, _p, _p, _i, _i, _i, _i, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _i, _i, _i, _p]),
+    "ast_mbt_gemm_f32": (_i, [_p, _p, _p, _i, _i, _i, _i, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _i, _i, _i, _i, _i,
+                              _p]),
     "ast_mbt_dw_f32": (_i, [_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
-    "ast_mbt_bn_fwd_f32": (_i, [_p, _i, _i, _ll, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p]),
-    "ast_mbt_bn_bwd_f32": (_i, [_p, _p, _i, _i, _ll, _p, _p, _p, _p, _p, _p, _p]),
+    "ast_mbt_bn_workspace_floats": (_ll, [_i, _i, _ll]),
+    "ast_mbt_bn_fwd_f32": (_i, [_p, _i, _i, _ll, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _ll, _p]),
+    "ast_mbt_bn_bwd_f32": (_i, [_p, _p, _i, _i, _ll, _p, _p, _p, _p, _p, _p, _p, _ll, _p]),
     "ast_mbt_eltwise_f32": (_i, [_i, _p, _p, _p, _ll, _i, _i, _p]),
     "ast_mbt_plane_f32": (_i, [_i, _p, _p, _p, _p, _p, _ll, _ll, _p]),
     "ast_mbt_se_fc_fwd_f32": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p]),

@@ -39,18 +39,23 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
 
 // ------------------------------------------------------------------------------------------------
 // GEMM: C[b][m][n] (+)= sum_k A[b][m][k] * B[b][k][n], general strides. 64x64 tile per workgroup,
-// 4 waves x 32x32 (v_mfma_f32_32x32x2_f32), K in chunks of 16 through LDS. grid.z = batch *
-// ksplit; with atomic != 0 partial sums are atomically added (C zeroed by the caller).
+// 4 waves x 32x32 (v_mfma_f32_32x32x2_f32), K in chunks of 32 through LDS; the next chunk's global
+// loads are issued before the current chunk's MFMAs (register prefetch). grid.z = batch * ksplit;
+// with atomic != 0 partial sums are atomically added (C zeroed by the caller).
+// Folding (NCHW 1x1 convs): foldN = P folds the image index into N (column n -> image n / P, pixel
+// n % P through the batch strides of B and C), so small planes still fill 64-wide tiles; foldK = P
+// folds it into K (the weight gradient's reduction over images x pixels). Both need batch == 1.
 // ------------------------------------------------------------------------------------------------
 struct GemmArgs {
   const float* A;
   const float* B;
   float* C;
   int64_t sAb, sAm, sAk, sBb, sBk, sBn, sCb, sCm, sCn;
-  int M, N, K, batch, ksplit, kchunk, accumulate, atomic;
+  int M, N, K, batch, ksplit, kchunk, accumulate, atomic, foldK, foldN;
 };
 
-constexpr int GT = 64, GK = 16, GP = GT + 4;
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+constexpr int GT = 64, GK = 32, GP = GT + 1, GL = GK * GT / kT;
 
 __global__ __launch_bounds__(kT) void gemm_kernel(GemmArgs a) {
   __shared__ float As[GK * GP];  // [k][m]
@@ -60,37 +65,99 @@ __global__ __launch_bounds__(kT) void gemm_kernel(GemmArgs a) {
   const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
   const int b = blockIdx.z / a.ksplit, ks = blockIdx.z % a.ksplit;
   const int kbeg = ks * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
+  // staging maps: the contiguous dimension runs along consecutive threads
+  const bool akf = a.sAk == 1, bnf = a.sBn == 1;
   const float* A = a.A + b * a.sAb;
   const float* B = a.B + b * a.sBb;
-  // staging maps: the contiguous dimension runs along consecutive threads
-  const bool a_kfast = a.sAk == 1, b_nfast = a.sBn == 1;
+  // fixed per-thread coordinates of the staged elements
+  const int a_k = tid & 31, a_m = tid >> 5;   // k-fast A: k = a_k, m = a_m + 8i
+  const int a_m2 = tid & 63, a_k2 = tid >> 6;  // m-fast A: m = a_m2, k = a_k2 + 4i
+  const int b_n = tid & 63, b_k = tid >> 6;    // n-fast B: n = b_n, k = b_k + 4i
+  const int b_k2 = tid & 31, b_n2 = tid >> 5;  // k-fast B: k = b_k2, n = b_n2 + 8i
+  int64_t bcol = 0;                             // n-fast B column offset (with the folded image)
+  if (bnf) {
+    const int gn = n0 + b_n;
+    if (a.foldN) {
+      const int bb = gn / a.foldN;
+      bcol = bb * a.sBb + (int64_t)(gn - bb * a.foldN);
+    } else {
+      bcol = gn;
+    }
+  }
+  f32x8 ra, rb;
+  auto load = [&](int k0) {
+    if (akf) {
+      const int gk = k0 + a_k;
+      int64_t kb = gk;
+      if (a.foldK) {
+        const int bb = gk / a.foldK;
+        kb = bb * a.sAb + (int64_t)(gk - bb * a.foldK);
+      }
+#pragma unroll
+      for (int i = 0; i < GL; ++i) {
+        const int gm = m0 + a_m + 8 * i;
+        ra[i] = (gk < kend && gm < a.M) ? A[gm * a.sAm + kb] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < GL; ++i) {
+        const int gk = k0 + a_k2 + 4 * i, gm = m0 + a_m2;
+        ra[i] = (gk < kend && gm < a.M) ? A[gm * a.sAm + (int64_t)gk * a.sAk] : 0.f;
+      }
+    }
+    if (bnf) {
+#pragma unroll
+      for (int i = 0; i < GL; ++i) {
+        const int gk = k0 + b_k + 4 * i;
+        rb[i] = (gk < kend && n0 + b_n < a.N) ? B[(int64_t)gk * a.sBk + bcol] : 0.f;
+      }
+    } else {
+      const int gk = k0 + b_k2;
+      int64_t kb = (int64_t)gk * a.sBk;
+      if (a.foldK) {
+        const int bb = gk / a.foldK;
+        kb = bb * a.sBb + (int64_t)(gk - bb * a.foldK) * a.sBk;
+      }
+#pragma unroll
+      for (int i = 0; i < GL; ++i) {
+        const int gn = n0 + b_n2 + 8 * i;
+        rb[i] = (gk < kend && gn < a.N) ? B[kb + gn * a.sBn] : 0.f;
+      }
+    }
+  };
   f32x16 acc = (f32x16){0.f};
+  if (kbeg < kend) load(kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += GK) {
 #pragma unroll
-    for (int i = 0; i < GK * GT / kT; ++i) {
-      const int e = tid + i * kT;
-      const int kk = a_kfast ? (e % GK) : (e / GT), mm = a_kfast ? (e / GK) : (e % GT);
-      const int gk = k0 + kk, gm = m0 + mm;
-      As[kk * GP + mm] = (gk < kend && gm < a.M) ? A[gm * a.sAm + (int64_t)gk * a.sAk] : 0.f;
-      const int kb = b_nfast ? (e / GT) : (e % GK), nb = b_nfast ? (e % GT) : (e / GK);
-      const int gkb = k0 + kb, gn = n0 + nb;
-      Bs[kb * GP + nb] = (gkb < kend && gn < a.N) ? B[(int64_t)gkb * a.sBk + gn * a.sBn] : 0.f;
+    for (int i = 0; i < GL; ++i) {
+      if (akf) As[a_k * GP + a_m + 8 * i] = ra[i];
+      else As[(a_k2 + 4 * i) * GP + a_m2] = ra[i];
+      if (bnf) Bs[(b_k + 4 * i) * GP + b_n] = rb[i];
+      else Bs[b_k2 * GP + b_n2 + 8 * i] = rb[i];
     }
     __syncthreads();
+    if (k0 + GK < kend) load(k0 + GK);
 #pragma unroll
     for (int kp = 0; kp < GK / 2; ++kp)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[(2 * kp + h) * GP + wm * 32 + r], Bs[(2 * kp + h) * GP + wn * 32 + r],
                                                  acc, 0, 0, 0);
     __syncthreads();
   }
-  float* C = a.C + b * a.sCb;
   const int n = n0 + wn * 32 + r;
   if (n >= a.N) return;
+  int64_t ccol;
+  if (a.foldN) {
+    const int bb = n / a.foldN;
+    ccol = bb * a.sCb + (int64_t)(n - bb * a.foldN) * a.sCn;
+  } else {
+    ccol = b * a.sCb + (int64_t)n * a.sCn;
+  }
+  float* C = a.C + ccol;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int m = m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
     if (m < a.M) {
-      float* c = C + m * a.sCm + n * a.sCn;
+      float* c = C + m * a.sCm;
       if (a.atomic) atomicAdd(c, acc[i]);
       else *c = a.accumulate ? *c + acc[i] : acc[i];
     }
@@ -98,195 +165,307 @@ __global__ __launch_bounds__(kT) void gemm_kernel(GemmArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// depthwise kxk conv with reflect padding p = (k-1)/2 (torch padding_mode="reflect"), stride s
+// depthwise kxk conv with reflect padding p = (k-1)/2 (torch padding_mode="reflect"), stride s.
+// The host guarantees p < size, so one reflection suffices. Flat 32-bit thread index over
+// planes x pixels (host-checked < 2^31).
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int refl(int i, int n) {
-  if (n == 1) return 0;
-  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * (n - 1) - i;
-  return i;
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * (n - 1) - i : i;
 }
 
-__global__ void dw_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ y, int64_t nc,
-                              int c, int h, int wd, int ho, int wo, int k, int s) {
-  const int p = (k - 1) / 2;
-  const int64_t tot = nc * ho * wo;
-  for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < tot; e += (int64_t)gridDim.x * kT) {
-    const int ox = (int)(e % wo);
-    const int64_t t = e / wo;
-    const int oy = (int)(t % ho);
-    const int64_t pl = t / ho;
-    const int ch = (int)(pl % c);
-    const float* xp = x + pl * h * wd;
-    const float* wc = w + (int64_t)ch * k * k;
-    float acc = 0.f;
-    for (int ky = 0; ky < k; ++ky) {
-      const int iy = refl(oy * s - p + ky, h);
-      for (int kx = 0; kx < k; ++kx) acc = fmaf(wc[ky * k + kx], xp[(int64_t)iy * wd + refl(ox * s - p + kx, wd)], acc);
-    }
-    y[e] = acc;
+template <int K, int S>
+__global__ __launch_bounds__(kT) void dw_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                    float* __restrict__ y, int total, int c, int h, int wd, int ho,
+                                                    int wo) {
+  constexpr int P = (K - 1) / 2;
+  const int e = blockIdx.x * kT + threadIdx.x;
+  if (e >= total) return;
+  const int hwo = ho * wo;
+  const int pl = e / hwo, rem = e - pl * hwo;
+  const int oy = rem / wo, ox = rem - oy * wo;
+  const float* xp = x + (int64_t)pl * h * wd;
+  const float* wc = w + (pl % c) * K * K;
+  int ix[K];
+#pragma unroll
+  for (int kx = 0; kx < K; ++kx) ix[kx] = refl(ox * S - P + kx, wd);
+  float acc = 0.f;
+#pragma unroll
+  for (int ky = 0; ky < K; ++ky) {
+    const float* row = xp + refl(oy * S - P + ky, h) * wd;
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx) acc = fmaf(wc[ky * K + kx], row[ix[kx]], acc);
   }
+  y[e] = acc;
 }
 
-// dx (zeroed by the caller) += scatter of g * w through the reflect map
-__global__ void dw_dgrad_kernel(const float* __restrict__ g, const float* __restrict__ w, float* __restrict__ dx,
-                                int64_t nc, int c, int h, int wd, int ho, int wo, int k, int s) {
-  const int p = (k - 1) / 2;
-  const int64_t tot = nc * ho * wo;
-  for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < tot; e += (int64_t)gridDim.x * kT) {
-    const int ox = (int)(e % wo);
-    const int64_t t = e / wo;
-    const int oy = (int)(t % ho);
-    const int64_t pl = t / ho;
-    const int ch = (int)(pl % c);
-    const float gv = g[e];
-    float* dp = dx + pl * h * wd;
-    const float* wc = w + (int64_t)ch * k * k;
-    for (int ky = 0; ky < k; ++ky) {
-      const int iy = refl(oy * s - p + ky, h);
-      for (int kx = 0; kx < k; ++kx) atomicAdd(dp + (int64_t)iy * wd + refl(ox * s - p + kx, wd), gv * wc[ky * k + kx]);
-    }
-  }
-}
-
-// dw[c][tap] += sum over one image's plane (grid = (c, n)); dw zeroed by the caller
-__global__ __launch_bounds__(kT) void dw_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ g,
-                                                      float* __restrict__ dw, int c, int h, int wd, int ho, int wo,
-                                                      int k, int s) {
-  __shared__ float sh[kT / 64];
-  const int ch = blockIdx.x, n = blockIdx.y, p = (k - 1) / 2;
-  const int64_t pl = (int64_t)n * c + ch;
-  const float* xp = x + pl * h * wd;
-  const float* gp = g + pl * ho * wo;
-  float acc[25];
+// dx[i][j] = sum over the padded positions q that reflect onto (i, j) and the taps t with
+// (q - t) = s * o for an output o of g[o] * w[t] -- a gather, no atomics. Per axis an input index
+// i has the interior preimage q = i + p, a top-pad preimage p - i (1 <= i <= p) and a bottom-pad
+// preimage 2(n-1) - i + p (n-1-p <= i <= n-2).
+template <int K, int S>
+__global__ __launch_bounds__(kT) void dw_dgrad_kernel(const float* __restrict__ g, const float* __restrict__ w,
+                                                      float* __restrict__ dx, int total, int c, int h, int wd, int ho,
+                                                      int wo) {
+  constexpr int P = (K - 1) / 2;
+  const int e = blockIdx.x * kT + threadIdx.x;
+  if (e >= total) return;
+  const int hw = h * wd;
+  const int pl = e / hw, rem = e - pl * hw;
+  const int iy = rem / wd, ix = rem - iy * wd;
+  const float* gp = g + (int64_t)pl * ho * wo;
+  const float* wc = w + (pl % c) * K * K;
+  float acc = 0.f;
 #pragma unroll
-  for (int t = 0; t < 25; ++t) acc[t] = 0.f;
-  for (int64_t e = threadIdx.x; e < (int64_t)ho * wo; e += kT) {
-    const int ox = (int)(e % wo), oy = (int)(e / wo);
-    const float gv = gp[e];
+  for (int ry = 0; ry < 3; ++ry) {
+    const bool vy = ry == 0 || (ry == 1 && iy >= 1 && iy <= P) || (ry == 2 && iy >= h - 1 - P && iy <= h - 2);
+    if (!vy) continue;
+    const int qy = ry == 0 ? iy + P : (ry == 1 ? P - iy : 2 * (h - 1) - iy + P);
 #pragma unroll
-    for (int ky = 0; ky < 5; ++ky) {
-      if (ky >= k) break;
-      const int iy = refl(oy * s - p + ky, h);
+    for (int ty = 0; ty < K; ++ty) {
+      const int t = qy - ty;
+      if (t < 0 || (t % S) != 0 || t / S >= ho) continue;
+      const float* grow = gp + (t / S) * wo;
 #pragma unroll
-      for (int kx = 0; kx < 5; ++kx) {
-        if (kx >= k) break;
-        acc[ky * 5 + kx] = fmaf(gv, xp[(int64_t)iy * wd + refl(ox * s - p + kx, wd)], acc[ky * 5 + kx]);
+      for (int rx = 0; rx < 3; ++rx) {
+        const bool vx = rx == 0 || (rx == 1 && ix >= 1 && ix <= P) || (rx == 2 && ix >= wd - 1 - P && ix <= wd - 2);
+        if (!vx) continue;
+        const int qx = rx == 0 ? ix + P : (rx == 1 ? P - ix : 2 * (wd - 1) - ix + P);
+#pragma unroll
+        for (int tx = 0; tx < K; ++tx) {
+          const int u = qx - tx;
+          if (u < 0 || (u % S) != 0 || u / S >= wo) continue;
+          acc = fmaf(grow[u / S], wc[ty * K + tx], acc);
+        }
       }
     }
   }
-  for (int ky = 0; ky < k; ++ky)
-    for (int kx = 0; kx < k; ++kx) {
-      const float t = block_sum(acc[ky * 5 + kx], sh);
-      if (threadIdx.x == 0) atomicAdd(dw + (int64_t)ch * k * k + ky * k + kx, t);
+  dx[e] = acc;
+}
+
+// dw[c][tap] += sum over a segment of one image's output plane (grid = (segments, n, c)); dw is
+// zeroed by the caller. The K*K partial sums are reduced across the wave by shuffles, across the
+// 4 waves through LDS.
+constexpr int DW_SEG = 8 * kT;
+
+template <int K, int S>
+__global__ __launch_bounds__(kT) void dw_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                      float* __restrict__ dw, int c, int h, int wd, int ho, int wo) {
+  constexpr int P = (K - 1) / 2, KK = K * K;
+  __shared__ float sh[4][KK];
+  const int ch = blockIdx.z, n = blockIdx.y;
+  const int64_t pl = (int64_t)n * c + ch;
+  const float* xp = x + pl * h * wd;
+  const float* gp = g + pl * ho * wo;
+  const int hwo = ho * wo;
+  const int beg = blockIdx.x * DW_SEG, end = min(hwo, beg + DW_SEG);
+  float acc[KK];
+#pragma unroll
+  for (int t = 0; t < KK; ++t) acc[t] = 0.f;
+  for (int e = beg + threadIdx.x; e < end; e += kT) {
+    const int oy = e / wo, ox = e - oy * wo;
+    const float gv = gp[e];
+    int ix[K];
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx) ix[kx] = refl(ox * S - P + kx, wd);
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const float* row = xp + refl(oy * S - P + ky, h) * wd;
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) acc[ky * K + kx] = fmaf(gv, row[ix[kx]], acc[ky * K + kx]);
     }
+  }
+#pragma unroll
+  for (int t = 0; t < KK; ++t) {
+    float v = acc[t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    acc[t] = v;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int t = 0; t < KK; ++t) sh[wave][t] = acc[t];
+  }
+  __syncthreads();
+  if (threadIdx.x < KK) {
+    const int t = threadIdx.x;
+    atomicAdd(dw + (int64_t)ch * KK + t, (sh[0][t] + sh[1][t]) + (sh[2][t] + sh[3][t]));
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
 // BatchNorm2d, training mode: batch mean and biased variance over (N, H, W) per channel,
 // y = (x - mean) * invstd * gamma + beta, invstd = 1/sqrt(var + eps); running statistics with
 // momentum and the unbiased variance (torch's batch_norm update).
+// Statistics in two steps: every (segment, image, channel) workgroup writes its count, mean and
+// M2 (sums shifted by the segment's first element against cancellation), then one thread per
+// channel merges them in double (Chan et al.'s pairwise update).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kT) void bn_stats_kernel(const float* __restrict__ x, int n, int c, int64_t hw, float eps,
-                                                      float momentum, float* __restrict__ mean,
-                                                      float* __restrict__ invstd, float* __restrict__ run_mean,
-                                                      float* __restrict__ run_var) {
+constexpr int BN_SEG = 16 * kT;
+
+__global__ __launch_bounds__(kT) void bn_part_stats_kernel(const float* __restrict__ x, int c, int64_t hw,
+                                                           float* __restrict__ part) {
   __shared__ float sh[kT / 64];
-  const int ch = blockIdx.x;
-  const int64_t m = (int64_t)n * hw;
-  float s = 0.f;
-  for (int b = 0; b < n; ++b) {
-    const float* xp = x + ((int64_t)b * c + ch) * hw;
-    for (int64_t i = threadIdx.x; i < hw; i += kT) s += xp[i];
+  const int sx = blockIdx.x, b = blockIdx.y, ch = blockIdx.z;
+  const float* xp = x + ((int64_t)b * c + ch) * hw + (int64_t)sx * BN_SEG;
+  const int len = (int)min((int64_t)BN_SEG, hw - (int64_t)sx * BN_SEG);
+  const float k0 = xp[0];
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < len; i += kT) {
+    const float d = xp[i] - k0;
+    s1 += d;
+    s2 = fmaf(d, d, s2);
   }
-  const float mu = block_sum(s, sh) / (float)m;
-  float q = 0.f;
-  for (int b = 0; b < n; ++b) {
-    const float* xp = x + ((int64_t)b * c + ch) * hw;
-    for (int64_t i = threadIdx.x; i < hw; i += kT) {
-      const float d = xp[i] - mu;
-      q = fmaf(d, d, q);
-    }
-  }
-  const float ss = block_sum(q, sh);
+  s1 = block_sum(s1, sh);
+  s2 = block_sum(s2, sh);
   if (threadIdx.x == 0) {
-    const float var = ss / (float)m;
-    mean[ch] = mu;
-    invstd[ch] = 1.0f / sqrtf(var + eps);
-    if (run_mean) {
-      run_mean[ch] = (1.f - momentum) * run_mean[ch] + momentum * mu;
-      run_var[ch] = (1.f - momentum) * run_var[ch] + momentum * (m > 1 ? ss / (float)(m - 1) : var);
+    const int S = gridDim.x * gridDim.y;
+    float* o = part + ((int64_t)ch * S + (int64_t)b * gridDim.x + sx) * 3;
+    const float inv = 1.0f / (float)len;
+    o[0] = (float)len;
+    o[1] = k0 + s1 * inv;
+    o[2] = fmaxf(s2 - s1 * s1 * inv, 0.f);
+  }
+}
+
+__global__ void bn_finalize_stats_kernel(const float* __restrict__ part, int S, int c, float eps, float momentum,
+                                         float* __restrict__ mean, float* __restrict__ invstd,
+                                         float* __restrict__ run_mean, float* __restrict__ run_var) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  const float* p = part + (int64_t)ch * S * 3;
+  double na = p[0], mu = p[1], m2 = p[2];
+  for (int i = 1; i < S; ++i) {
+    const double nb = p[3 * i], mb = p[3 * i + 1], m2b = p[3 * i + 2];
+    const double nt = na + nb, d = mb - mu;
+    mu += d * nb / nt;
+    m2 += m2b + d * d * na * nb / nt;
+    na = nt;
+  }
+  const double var = m2 / na;
+  mean[ch] = (float)mu;
+  invstd[ch] = 1.0f / sqrtf((float)var + eps);
+  if (run_mean) {
+    run_mean[ch] = (1.f - momentum) * run_mean[ch] + momentum * (float)mu;
+    run_var[ch] = (1.f - momentum) * run_var[ch] + momentum * (float)(na > 1 ? m2 / (na - 1) : var);
+  }
+}
+
+// grid (chunks of 4*kT pixels, planes (strided by gridDim.y))
+__global__ __launch_bounds__(kT) void bn_apply_kernel(const float* __restrict__ x, int c, int64_t hw, int planes,
+                                                      const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      float* __restrict__ y) {
+  for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
+    const int ch = pl % c;
+    const float sc = invstd[ch] * (gamma ? gamma[ch] : 1.f), mu = mean[ch], bt = beta ? beta[ch] : 0.f;
+    const float* xp = x + (int64_t)pl * hw;
+    float* yp = y + (int64_t)pl * hw;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = (int64_t)blockIdx.x * 4 * kT + j * kT + threadIdx.x;
+      if (i < hw) yp[i] = (xp[i] - mu) * sc + bt;
     }
   }
 }
 
-__global__ void bn_apply_kernel(const float* __restrict__ x, int c, int64_t hw, int64_t total, const float* __restrict__ mean,
-                                const float* __restrict__ invstd, const float* __restrict__ gamma,
-                                const float* __restrict__ beta, float* __restrict__ y) {
-  for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
-    const int ch = (int)((e / hw) % c);
-    y[e] = (x[e] - mean[ch]) * invstd[ch] * (gamma ? gamma[ch] : 1.f) + (beta ? beta[ch] : 0.f);
-  }
-}
-
-// per channel: sum(dy) -> dbeta, sum(dy * xhat) -> dgamma
-__global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                                           int n, int c, int64_t hw, const float* __restrict__ mean,
-                                                           const float* __restrict__ invstd, float* __restrict__ sdy,
-                                                           float* __restrict__ sdyx) {
+// per (segment, image, channel): sum(dy), sum(dy * xhat)
+__global__ __launch_bounds__(kT) void bn_part_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                         int c, int64_t hw, const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd, float* __restrict__ part) {
   __shared__ float sh[kT / 64];
-  const int ch = blockIdx.x;
+  const int sx = blockIdx.x, b = blockIdx.y, ch = blockIdx.z;
+  const int64_t o = ((int64_t)b * c + ch) * hw + (int64_t)sx * BN_SEG;
+  const int len = (int)min((int64_t)BN_SEG, hw - (int64_t)sx * BN_SEG);
   const float mu = mean[ch], is = invstd[ch];
-  float a = 0.f, b2 = 0.f;
-  for (int b = 0; b < n; ++b) {
-    const int64_t o = ((int64_t)b * c + ch) * hw;
-    for (int64_t i = threadIdx.x; i < hw; i += kT) {
-      const float g = dy[o + i];
-      a += g;
-      b2 = fmaf(g, (x[o + i] - mu) * is, b2);
-    }
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < len; i += kT) {
+    const float gv = dy[o + i];
+    s1 += gv;
+    s2 = fmaf(gv, (x[o + i] - mu) * is, s2);
   }
-  const float A = block_sum(a, sh);
-  const float Bv = block_sum(b2, sh);
+  s1 = block_sum(s1, sh);
+  s2 = block_sum(s2, sh);
   if (threadIdx.x == 0) {
-    sdy[ch] = A;
-    sdyx[ch] = Bv;
+    const int S = gridDim.x * gridDim.y;
+    float* p = part + ((int64_t)ch * S + (int64_t)b * gridDim.x + sx) * 2;
+    p[0] = s1;
+    p[1] = s2;
   }
 }
 
-__global__ void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy, int c, int64_t hw,
-                                    int64_t total, int64_t m, const float* __restrict__ mean,
-                                    const float* __restrict__ invstd, const float* __restrict__ gamma,
-                                    const float* __restrict__ sdy, const float* __restrict__ sdyx,
-                                    float* __restrict__ dx) {
-  for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
-    const int ch = (int)((e / hw) % c);
-    const float is = invstd[ch], xh = (x[e] - mean[ch]) * is;
-    const float gm = gamma ? gamma[ch] : 1.f;
-    dx[e] = gm * is * (dy[e] - sdy[ch] / (float)m - xh * sdyx[ch] / (float)m);
+__global__ void bn_finalize_bwd_kernel(const float* __restrict__ part, int S, int c, float* __restrict__ sdy,
+                                       float* __restrict__ sdyx) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  const float* p = part + (int64_t)ch * S * 2;
+  double a = 0.0, b = 0.0;
+  for (int i = 0; i < S; ++i) {
+    a += p[2 * i];
+    b += p[2 * i + 1];
+  }
+  sdy[ch] = (float)a;
+  sdyx[ch] = (float)b;
+}
+
+__global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                          int c, int64_t hw, int planes, float inv_m,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ sdy,
+                                                          const float* __restrict__ sdyx, float* __restrict__ dx) {
+  for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
+    const int ch = pl % c;
+    const float is = invstd[ch], mu = mean[ch], gm = (gamma ? gamma[ch] : 1.f) * is;
+    const float a = sdy[ch] * inv_m, bq = sdyx[ch] * inv_m;
+    const int64_t base = (int64_t)pl * hw;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = (int64_t)blockIdx.x * 4 * kT + j * kT + threadIdx.x;
+      if (i < hw) {
+        const float xh = (x[base + i] - mu) * is;
+        dx[base + i] = gm * (dy[base + i] - a - xh * bq);
+      }
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------------
 // elementwise
 // ------------------------------------------------------------------------------------------------
-__global__ void hswish_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n) {
-  for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < n; e += (int64_t)gridDim.x * kT) {
-    const float v = x[e];
-    y[e] = v * fminf(fmaxf(v + 3.f, 0.f), 6.f) / 6.f;
-  }
+// op 0 hardswish(a), 1 hardswish backward (x = a, g = b; torch: x < -3: 0; x <= 3: g (x/3 + 1/2);
+// else g), 2 a + b. Four elements per thread, as one 16-byte access when the host saw n % 4 == 0
+// and 16-byte aligned pointers.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int OP>
+__device__ __forceinline__ float elt(float a, float b) {
+  if (OP == 0) return a * fminf(fmaxf(a + 3.f, 0.f), 6.f) / 6.f;
+  if (OP == 1) return a < -3.f ? 0.f : (a <= 3.f ? b * (a / 3.f + 0.5f) : b);
+  return a + b;
 }
 
-// torch hardswish_backward: x < -3: 0; x <= 3: g * (x / 3 + 0.5); else g
-__global__ void hswish_bwd_kernel(const float* __restrict__ x, const float* __restrict__ g, float* __restrict__ dx,
-                                  int64_t n) {
-  for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < n; e += (int64_t)gridDim.x * kT) {
-    const float v = x[e];
-    dx[e] = v < -3.f ? 0.f : (v <= 3.f ? g[e] * (v / 3.f + 0.5f) : g[e]);
+template <int OP, bool V4>
+__global__ __launch_bounds__(kT) void eltwise_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                     float* __restrict__ y, int64_t n) {
+  const int64_t i0 = ((int64_t)blockIdx.x * kT + threadIdx.x) * 4;
+  if (V4) {
+    if (i0 >= n) return;
+    const f32x4 va = *(const f32x4*)(a + i0);
+    const f32x4 vb = OP == 0 ? va : *(const f32x4*)(b + i0);
+    f32x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = elt<OP>(va[j], vb[j]);
+    *(f32x4*)(y + i0) = r;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = i0 + j;
+      if (i < n) y[i] = elt<OP>(a[i], OP == 0 ? 0.f : b[i]);
+    }
   }
-}
-
-__global__ void add_kernel(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ y, int64_t n) {
-  for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < n; e += (int64_t)gridDim.x * kT) y[e] = a[e] + b[e];
 }
 
 __global__ void up2_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t planes, int h, int w) {
@@ -325,12 +504,20 @@ __global__ __launch_bounds__(kT) void plane_dot_kernel(const float* __restrict__
   if (threadIdx.x == 0) out[p] = t * scale;
 }
 
-// y = x * gate[plane] (+ gadd[plane] when given: the SE input gradient dy*g + dpool/hw)
-__global__ void plane_scale_kernel(const float* __restrict__ x, const float* __restrict__ gate,
-                                   const float* __restrict__ gadd, int64_t hw, int64_t total, float* __restrict__ y) {
-  for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
-    const int64_t p = e / hw;
-    y[e] = x[e] * gate[p] + (gadd ? gadd[p] : 0.f);
+// y = x * gate[plane] (+ gadd[plane] when given: the SE input gradient dy*g + dpool/hw);
+// grid (chunks of 4*kT pixels, planes strided by gridDim.y)
+__global__ __launch_bounds__(kT) void plane_scale_kernel(const float* __restrict__ x, const float* __restrict__ gate,
+                                                         const float* __restrict__ gadd, int64_t hw, int64_t planes,
+                                                         float* __restrict__ y) {
+  for (int64_t p = blockIdx.y; p < planes; p += gridDim.y) {
+    const float gv = gate[p], av = gadd ? gadd[p] : 0.f;
+    const float* xp = x + p * hw;
+    float* yp = y + p * hw;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = (int64_t)blockIdx.x * 4 * kT + j * kT + threadIdx.x;
+      if (i < hw) yp[i] = fmaf(xp[i], gv, av);
+    }
   }
 }
 
@@ -404,23 +591,48 @@ __global__ __launch_bounds__(kT) void se_fc_bwd_kernel(const float* __restrict__
   }
 }
 
+dim3 plane_grid(int64_t hw, int64_t planes) {
+  return dim3((unsigned)((hw + 4 * kT - 1) / (4 * kT)), (unsigned)(planes < 65535 ? planes : 65535));
+}
+
+template <int OP>
+void launch_eltwise(const float* a, const float* b, float* y, int64_t n, hipStream_t st) {
+  const bool v4 = (n & 3) == 0 && (((uintptr_t)a | (uintptr_t)(b ? b : a) | (uintptr_t)y) & 15) == 0;
+  const dim3 grid((unsigned)((n + 4 * kT - 1) / (4 * kT)));
+  if (v4) hipLaunchKernelGGL((eltwise_kernel<OP, true>), grid, dim3(kT), 0, st, a, b, y, n);
+  else hipLaunchKernelGGL((eltwise_kernel<OP, false>), grid, dim3(kT), 0, st, a, b, y, n);
+}
+
 }  // namespace
 
 extern "C" {
 
 int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int K, int batch, long long sAb,
                      long long sAm, long long sAk, long long sBb, long long sBk, long long sBn, long long sCb,
-                     long long sCm, long long sCn, int ksplit, int accumulate, int atomic, void* stream) {
+                     long long sCm, long long sCn, int ksplit, int accumulate, int atomic, int foldK, int foldN,
+                     void* stream) {
   if (!A || !B || !C) return AST_E_NULLPTR;
-  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || ksplit <= 0) return AST_E_SHAPE;
+  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || ksplit <= 0 || foldK < 0 || foldN < 0) return AST_E_SHAPE;
   if (((int64_t)M + GT - 1) / GT > 65535 || (int64_t)batch * ksplit > 65535) return AST_E_SHAPE;
+  if ((foldK || foldN) && (batch != 1 || (foldK && foldN))) return AST_E_SHAPE;
+  if (foldK && (sAk != 1 || sBk != 1 || K % foldK)) return AST_E_UNSUPPORTED;  // both operands k-contiguous
+  if (foldN && (sBn != 1 || N % foldN)) return AST_E_UNSUPPORTED;
   if (ksplit > 1 || (sCb == 0 && batch > 1)) atomic = 1;  // partial sums meet in C
-  GemmArgs a{A, B, C, sAb, sAm, sAk, sBb, sBk, sBn, sCb, sCm, sCn, M, N, K, batch, ksplit, 0, accumulate, atomic};
+  GemmArgs a{A, B, C, sAb, sAm, sAk, sBb, sBk, sBn, sCb, sCm, sCn, M, N, K, batch, ksplit, 0, accumulate, atomic,
+             foldK, foldN};
   a.kchunk = ((K + ksplit - 1) / ksplit + GK - 1) / GK * GK;
   const dim3 grid((unsigned)((N + GT - 1) / GT), (unsigned)((M + GT - 1) / GT), (unsigned)(batch * ksplit));
   hipLaunchKernelGGL(gemm_kernel, grid, dim3(kT), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
+
+#define AST_DW_DISPATCH(KERNEL, grid, ...)                                                          \
+  do {                                                                                              \
+    if (k == 3 && s == 1) hipLaunchKernelGGL((KERNEL<3, 1>), grid, dim3(kT), 0, st, __VA_ARGS__);   \
+    else if (k == 3) hipLaunchKernelGGL((KERNEL<3, 2>), grid, dim3(kT), 0, st, __VA_ARGS__);        \
+    else if (s == 1) hipLaunchKernelGGL((KERNEL<5, 1>), grid, dim3(kT), 0, st, __VA_ARGS__);        \
+    else hipLaunchKernelGGL((KERNEL<5, 2>), grid, dim3(kT), 0, st, __VA_ARGS__);                    \
+  } while (0)
 
 int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, float* out, int n, int c, int h, int wd,
                    int k, int s, void* stream) {
@@ -429,47 +641,59 @@ int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, flo
   const int p = (k - 1) / 2;
   if (p >= h || p >= wd) return AST_E_SHAPE;  // reflect padding needs pad < size
   const int ho = (h + 2 * p - k) / s + 1, wo = (wd + 2 * p - k) / s + 1;
-  hipStream_t st = (hipStream_t)stream;
   const int64_t nc = (int64_t)n * c;
+  if (nc * h * wd >= (1LL << 31) || n > 65535 || c > 65535) return AST_E_SHAPE;  // 32-bit flat indices
+  hipStream_t st = (hipStream_t)stream;
   if (mode == 0) {
-    hipLaunchKernelGGL(dw_fwd_kernel, dim3(grid_for(nc * ho * wo)), dim3(kT), 0, st, x, w, out, nc, c, h, wd, ho, wo, k, s);
+    const int total = (int)(nc * ho * wo);
+    AST_DW_DISPATCH(dw_fwd_kernel, dim3((total + kT - 1) / kT), x, w, out, total, c, h, wd, ho, wo);
   } else if (mode == 1) {
-    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)(nc * h * wd), st);
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(dw_dgrad_kernel, dim3(grid_for(nc * ho * wo)), dim3(kT), 0, st, g, w, out, nc, c, h, wd, ho, wo,
-                       k, s);
+    const int total = (int)(nc * h * wd);
+    AST_DW_DISPATCH(dw_dgrad_kernel, dim3((total + kT - 1) / kT), g, w, out, total, c, h, wd, ho, wo);
   } else {
     hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)c * k * k, st);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(dw_wgrad_kernel, dim3(c, n), dim3(kT), 0, st, x, g, out, c, h, wd, ho, wo, k, s);
+    const dim3 grid((unsigned)((ho * wo + DW_SEG - 1) / DW_SEG), (unsigned)n, (unsigned)c);
+    AST_DW_DISPATCH(dw_wgrad_kernel, grid, x, g, out, c, h, wd, ho, wo);
   }
   return (int)hipGetLastError();
 }
 
+long long ast_mbt_bn_workspace_floats(int n, int c, long long hw) {
+  if (n <= 0 || c <= 0 || hw <= 0) return 0;
+  return 3LL * c * n * ((hw + BN_SEG - 1) / BN_SEG);
+}
+
 int ast_mbt_bn_fwd_f32(const float* x, int n, int c, long long hw, const float* gamma, const float* beta, float eps,
                        float momentum, float* mean, float* invstd, float* run_mean, float* run_var, float* y,
-                       void* stream) {
-  if (!x || !mean || !invstd || !y) return AST_E_NULLPTR;
-  if (n <= 0 || c <= 0 || hw <= 0) return AST_E_SHAPE;
+                       float* workspace, long long workspace_floats, void* stream) {
+  if (!x || !mean || !invstd || !y || !workspace) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hw <= 0 || n > 65535 || c > 65535) return AST_E_SHAPE;
+  if (workspace_floats < ast_mbt_bn_workspace_floats(n, c, hw)) return AST_E_SHAPE;  // workspace too small
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(c), dim3(kT), 0, st, x, n, c, (int64_t)hw, eps, momentum, mean, invstd,
-                     run_mean, run_var);
-  const int64_t total = (int64_t)n * c * hw;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(total)), dim3(kT), 0, st, x, c, (int64_t)hw, total, mean, invstd,
-                     gamma, beta, y);
+  const int segs = (int)((hw + BN_SEG - 1) / BN_SEG);
+  hipLaunchKernelGGL(bn_part_stats_kernel, dim3(segs, n, c), dim3(kT), 0, st, x, c, (int64_t)hw, workspace);
+  hipLaunchKernelGGL(bn_finalize_stats_kernel, dim3((c + 63) / 64), dim3(64), 0, st, workspace, segs * n, c, eps,
+                     momentum, mean, invstd, run_mean, run_var);
+  hipLaunchKernelGGL(bn_apply_kernel, plane_grid(hw, (int64_t)n * c), dim3(kT), 0, st, x, c, (int64_t)hw, n * c, mean,
+                     invstd, gamma, beta, y);
   return (int)hipGetLastError();
 }
 
 int ast_mbt_bn_bwd_f32(const float* x, const float* dy, int n, int c, long long hw, const float* mean,
-                       const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dx, void* stream) {
-  if (!x || !dy || !mean || !invstd || !dgamma || !dbeta || !dx) return AST_E_NULLPTR;
-  if (n <= 0 || c <= 0 || hw <= 0) return AST_E_SHAPE;
+                       const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dx,
+                       float* workspace, long long workspace_floats, void* stream) {
+  if (!x || !dy || !mean || !invstd || !dgamma || !dbeta || !dx || !workspace) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hw <= 0 || n > 65535 || c > 65535) return AST_E_SHAPE;
+  if (workspace_floats < ast_mbt_bn_workspace_floats(n, c, hw)) return AST_E_SHAPE;  // workspace too small
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(c), dim3(kT), 0, st, x, dy, n, c, (int64_t)hw, mean, invstd, dbeta,
+  const int segs = (int)((hw + BN_SEG - 1) / BN_SEG);
+  hipLaunchKernelGGL(bn_part_bwd_kernel, dim3(segs, n, c), dim3(kT), 0, st, x, dy, c, (int64_t)hw, mean, invstd,
+                     workspace);
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((c + 63) / 64), dim3(64), 0, st, workspace, segs * n, c, dbeta,
                      dgamma);
-  const int64_t total = (int64_t)n * c * hw;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total)), dim3(kT), 0, st, x, dy, c, (int64_t)hw, total,
-                     (int64_t)n * hw, mean, invstd, gamma, dbeta, dgamma, dx);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, plane_grid(hw, (int64_t)n * c), dim3(kT), 0, st, x, dy, c, (int64_t)hw,
+                     n * c, 1.0f / (float)((int64_t)n * hw), mean, invstd, gamma, dbeta, dgamma, dx);
   return (int)hipGetLastError();
 }
 
@@ -480,9 +704,14 @@ int ast_mbt_eltwise_f32(int op, const float* a, const float* b, float* y, long l
   if (n <= 0) return AST_E_SHAPE;
   hipStream_t st = (hipStream_t)stream;
   switch (op) {
-    case 0: hipLaunchKernelGGL(hswish_kernel, dim3(grid_for(n)), dim3(kT), 0, st, a, y, (int64_t)n); break;
-    case 1: hipLaunchKernelGGL(hswish_bwd_kernel, dim3(grid_for(n)), dim3(kT), 0, st, a, b, y, (int64_t)n); break;
-    case 2: hipLaunchKernelGGL(add_kernel, dim3(grid_for(n)), dim3(kT), 0, st, a, b, y, (int64_t)n); break;
+    case 0:
+    case 1:
+    case 2:
+      if (n >= (1LL << 40)) return AST_E_SHAPE;
+      if (op == 0) launch_eltwise<0>(a, nullptr, y, (int64_t)n, st);
+      else if (op == 1) launch_eltwise<1>(a, b, y, (int64_t)n, st);
+      else launch_eltwise<2>(a, b, y, (int64_t)n, st);
+      break;
     case 3:
       if (h <= 0 || w <= 0) return AST_E_SHAPE;
       hipLaunchKernelGGL(up2_kernel, dim3(grid_for(n * 4 * h * w)), dim3(kT), 0, st, a, y, (int64_t)n, h, w);
@@ -506,8 +735,8 @@ int ast_mbt_plane_f32(int op, const float* x, const float* y, const float* gate,
     hipLaunchKernelGGL(plane_dot_kernel, dim3((unsigned)planes), dim3(kT), 0, st, x, op == 1 ? y : nullptr,
                        (int64_t)hw, op == 0 ? 1.0f / (float)hw : 1.0f, out);
   else if (op == 2)
-    hipLaunchKernelGGL(plane_scale_kernel, dim3(grid_for(planes * hw)), dim3(kT), 0, st, x, gate, gadd, (int64_t)hw,
-                       (int64_t)(planes * hw), out);
+    hipLaunchKernelGGL(plane_scale_kernel, plane_grid(hw, planes), dim3(kT), 0, st, x, gate, gadd, (int64_t)hw,
+                       (int64_t)planes, out);
   else
     return AST_E_UNSUPPORTED;
   return (int)hipGetLastError();

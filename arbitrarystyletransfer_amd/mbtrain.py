@@ -29,14 +29,18 @@ def _f32(t, name):
     return t.contiguous()
 
 
-def gemm(A, B, C, M, N, K, batch, sA, sB, sC, ksplit=1, accumulate=False):
-    """C[b][m][n] (+)= sum_k A[b][m][k] B[b][k][n]; sA/sB/sC = (batch, row, col) element strides."""
-    check(ops._timed("mbgemm", 2 * M * N * K * batch, C.device, lambda: lib().ast_mbt_gemm_f32(
-        ptr(A), ptr(B), ptr(C), M, N, K, batch, *sA, *sB, *sC, ksplit, int(accumulate), 0, _s(C))), "gemm")
+def gemm(A, B, C, M, N, K, batch, sA, sB, sC, ksplit=1, accumulate=False, fold_k=0, fold_n=0, role=""):
+    """C[b][m][n] (+)= sum_k A[b][m][k] B[b][k][n]; sA/sB/sC = (batch, row, col) element strides.
+    fold_n / fold_k = P: the image index is folded into N / K (batch 1; see ast_hip.h)."""
+    check(ops._timed(f"mbgemm {role} {M}x{N}x{K}", 2 * M * N * K * batch, C.device, lambda: lib().ast_mbt_gemm_f32(
+        ptr(A), ptr(B), ptr(C), M, N, K, batch, *sA, *sB, *sC, ksplit, int(accumulate), 0, fold_k, fold_n, _s(C))),
+        "gemm")
 
 
-def _ksplit(p):
-    return max(1, min(64, p // 4096))
+def _ksplit(m, n, k):
+    """Split the weight gradient's long reduction so ~512 workgroups run, chunks >= 512 deep."""
+    tiles = -(-m // 64) * -(-n // 64)
+    return max(1, min(-(-512 // tiles), k // 512))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -51,11 +55,12 @@ class PwConvFn(torch.autograd.Function):
         cout, cin = weight.shape[0], weight.shape[1]
         wt = weight.detach().reshape(cout, cin).contiguous()
         y = torch.empty((n, cout, h, w), device=x.device, dtype=torch.float32)
-        gemm(wt, x, y, cout, P, c1, n, (0, cin, 1), (c1 * P, P, 1), (cout * P, P, 1))
+        gemm(wt, x, y, cout, n * P, c1, 1, (0, cin, 1), (c1 * P, P, 1), (cout * P, P, 1), fold_n=P, role="fwd")
         if x2 is not None:
             x2 = _f32(x2, "x2")
             c2 = x2.shape[1]
-            gemm(wt[:, c1:], x2, y, cout, P, c2, n, (0, cin, 1), (c2 * P, P, 1), (cout * P, P, 1), accumulate=True)
+            gemm(wt[:, c1:], x2, y, cout, n * P, c2, 1, (0, cin, 1), (c2 * P, P, 1), (cout * P, P, 1), accumulate=True,
+                 fold_n=P, role="fwd")
         ctx.save_for_backward(x, x2 if x2 is not None else x, wt)
         ctx.has_x2 = x2 is not None
         ctx.wshape = weight.shape
@@ -77,7 +82,8 @@ class PwConvFn(torch.autograd.Function):
             d = None
             if ctx.needs_input_grad[0 if off == 0 else 1]:
                 d = torch.empty_like(xi)
-                gemm(wt[:, off:], g, d, ci, P, cout, n, (0, 1, cin), (cout * P, P, 1), (ci * P, P, 1))
+                gemm(wt[:, off:], g, d, ci, n * P, cout, 1, (0, 1, cin), (cout * P, P, 1), (ci * P, P, 1),
+                     fold_n=P, role="dgrad")
             grads.append(d)
         dx = grads[0]
         if ctx.has_x2:
@@ -86,8 +92,8 @@ class PwConvFn(torch.autograd.Function):
             dw = torch.zeros((cout, cin), device=g.device, dtype=torch.float32)
             for xi, off in parts:
                 ci = xi.shape[1]
-                gemm(g, xi, dw[:, off:], cout, ci, P, n, (cout * P, P, 1), (ci * P, 1, P), (0, cin, 1),
-                     ksplit=_ksplit(P))
+                gemm(g, xi, dw[:, off:], cout, ci, n * P, 1, (cout * P, P, 1), (ci * P, 1, P), (0, cin, 1),
+                     ksplit=_ksplit(cout, ci, n * P), fold_k=P, role="wgrad")
             dw = dw.reshape(ctx.wshape)
         return dx, dx2, dw
 
@@ -125,6 +131,10 @@ class DwConvFn(torch.autograd.Function):
         return dx, dw, None, None
 
 
+def _bn_workspace(x, n, c, hw):
+    return torch.empty((max(1, lib().ast_mbt_bn_workspace_floats(n, c, hw)),), device=x.device, dtype=torch.float32)
+
+
 class BatchNormTrainFn(torch.autograd.Function):
     """BatchNorm2d.forward in training mode (batch statistics; running stats updated in place)."""
 
@@ -135,11 +145,13 @@ class BatchNormTrainFn(torch.autograd.Function):
         mean = torch.empty((c,), device=x.device, dtype=torch.float32)
         invstd = torch.empty_like(mean)
         y = torch.empty_like(x)
+        ws = _bn_workspace(x, n, c, h * w)
         track = bn.track_running_stats and bn.running_mean is not None
         momentum = bn.momentum if bn.momentum is not None else 0.1
         check(lib().ast_mbt_bn_fwd_f32(ptr(x), n, c, h * w, ptr(gamma), ptr(beta), float(bn.eps), float(momentum),
                                        ptr(mean), ptr(invstd), ptr(bn.running_mean) if track else None,
-                                       ptr(bn.running_var) if track else None, ptr(y), _s(x)), "batch norm")
+                                       ptr(bn.running_var) if track else None, ptr(y), ptr(ws), ws.numel(), _s(x)),
+              "batch norm")
         if track:
             bn.num_batches_tracked.add_(1)   # bookkeeping counter (torch does the same host-side increment)
         ctx.save_for_backward(x, gamma, mean, invstd)
@@ -153,8 +165,9 @@ class BatchNormTrainFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         dgamma = torch.empty_like(mean)
         dbeta = torch.empty_like(mean)
+        ws = _bn_workspace(x, n, c, h * w)
         check(lib().ast_mbt_bn_bwd_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma), ptr(dgamma),
-                                       ptr(dbeta), ptr(dx), _s(g)), "batch norm backward")
+                                       ptr(dbeta), ptr(dx), ptr(ws), ws.numel(), _s(g)), "batch norm backward")
         return dx, dgamma, dbeta, None
 
 

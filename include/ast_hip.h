@@ -369,11 +369,13 @@ int ast_aug_blur_f32(const float* src, int c, int h, int w, const float* taps, i
 
 /* C[b][m][n] (+)= sum_k A[b][m][k] B[b][k][n] with element strides (1x1 convs and their grads).
  * ksplit > 1 splits K across workgroups; partial sums are then atomically added (as when C is
- * shared across the batch, sCb == 0): C must hold the starting value (zero it to overwrite). */
+ * shared across the batch, sCb == 0): C must hold the starting value (zero it to overwrite).
+ * foldN = P > 0 (batch 1, B n-contiguous): column n is pixel n % P of image n / P, reached through
+ * the image strides sBb / sCb; foldK = P > 0 (batch 1, A and B k-contiguous): the same for K. */
 int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int K, int batch,
                      long long sAb, long long sAm, long long sAk, long long sBb, long long sBk,
                      long long sBn, long long sCb, long long sCm, long long sCn, int ksplit,
-                     int accumulate, int atomic, void* stream);
+                     int accumulate, int atomic, int foldK, int foldN, void* stream);
 
 /* Depthwise k x k conv (k 3|5, stride 1|2, reflect pad (k-1)/2; mobilenetv2.py:148-149, :116-117):
  * mode 0 out = conv(x, w); 1 out = dx from g (overwritten); 2 out = dw [c][k*k] from x, g. */
@@ -381,13 +383,17 @@ int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, flo
                    int c, int h, int wd, int k, int s, void* stream);
 
 /* BatchNorm2d in training mode (batch statistics, biased var + eps; running stats updated with
- * momentum and the unbiased variance when run_mean/run_var are given). mean/invstd [c] saved. */
+ * momentum and the unbiased variance when run_mean/run_var are given). mean/invstd [c] saved.
+ * workspace: ast_mbt_bn_workspace_floats(n, c, hw) floats of per-segment partial statistics. */
+long long ast_mbt_bn_workspace_floats(int n, int c, long long hw);
 int ast_mbt_bn_fwd_f32(const float* x, int n, int c, long long hw, const float* gamma,
                        const float* beta, float eps, float momentum, float* mean, float* invstd,
-                       float* run_mean, float* run_var, float* y, void* stream);
+                       float* run_mean, float* run_var, float* y, float* workspace,
+                       long long workspace_floats, void* stream);
 int ast_mbt_bn_bwd_f32(const float* x, const float* dy, int n, int c, long long hw,
                        const float* mean, const float* invstd, const float* gamma, float* dgamma,
-                       float* dbeta, float* dx, void* stream);
+                       float* dbeta, float* dx, float* workspace, long long workspace_floats,
+                       void* stream);
 
 /* op 0 y = hardswish(a); 1 y = hardswish'(a) * b; 2 y = a + b; 3 y = nearest-upsample x2 of a
  * (n planes of h x w); 4 its backward (a = grad of the 2h x 2w planes). */

@@ -34,6 +34,32 @@ def shapes(batch):
     return out
 
 
+def ae_shapes(batch=16, size=160):
+    """The conv3x3 launches of one AutoEncoder training step (bench.py --mode ae-train: the VGG
+    loss network's forward passes and input-gradient convs), captured from a live step."""
+    from arbitrarystyletransfer_amd import models
+    from arbitrarystyletransfer_amd.train import AutoencoderTrainer, default_ae_args
+    seen = []
+    orig = ops.conv3x3
+
+    def spy(x, w_packed, bias, cout, *, upsample=1, pad_mode="zeros", want_pool=False, x2=None, **kw):
+        n = int(x.shape[0]) + (int(x2.shape[0]) if x2 is not None else 0)
+        shp = (n, int(x.shape[1]), int(x.shape[2]), int(x.shape[3]), cout, upsample, pad_mode, want_pool)
+        if shp not in seen:
+            seen.append(shp)
+        return orig(x, w_packed, bias, cout, upsample=upsample, pad_mode=pad_mode, want_pool=want_pool, x2=x2, **kw)
+
+    ops.conv3x3 = spy
+    try:
+        tr = AutoencoderTrainer(default_ae_args(batch_size=batch), device="cuda",
+                                model=models.AutoEncoder().load_live_init())
+        tr.train_step(torch.from_numpy(synth.image(901, (batch, 3, size, size))).cuda(), record=False)
+        torch.cuda.synchronize()
+    finally:
+        ops.conv3x3 = orig
+    return seen
+
+
 def key(n, cin, h, w, cout, up, pad, pool):
     return f"{n}x{cin}x{h}x{w}->{cout} up{up} {pad}{' pool' if pool else ''}"
 
@@ -68,7 +94,8 @@ def main():
     if os.path.exists(path):
         table = json.load(open(path))
     report = []
-    for shp in shapes(batch):
+    todo = ae_shapes() if os.environ.get("TUNE_AE") else shapes(batch)
+    for shp in todo:
         n, cin, h, w, cout, up, pad, pool = shp
         x = torch.from_numpy(synth.image(5, (n, cin, h, w))).to(dev)
         wt = torch.from_numpy(synth.conv_weight(6, cout, cin, 3)).to(dev)

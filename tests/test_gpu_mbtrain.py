@@ -36,13 +36,14 @@ def pair(*shape, scale=1.0):
     return t.clone().requires_grad_(), t.cuda().requires_grad_()
 
 
-@pytest.mark.parametrize("split", [False, True])
-def test_pw_conv(split):
+@pytest.mark.parametrize("split,shape,cout", [(False, (2, 24, 9, 13), 40), (True, (2, 24, 9, 13), 40),
+                                              (False, (3, 96, 5, 5), 130), (True, (4, 40, 20, 20), 72)])
+def test_pw_conv(split, shape, cout):
     torch.manual_seed(0)
-    xc, xg = pair(2, 24, 9, 13)
-    wc, wg = pair(40, 24 + (8 if split else 0), 1, 1)
+    xc, xg = pair(*shape)
+    wc, wg = pair(cout, shape[1] + (8 if split else 0), 1, 1)
     if split:
-        x2c, x2g = pair(2, 8, 9, 13)
+        x2c, x2g = pair(shape[0], 8, *shape[2:])
         yc = F.conv2d(torch.cat((xc, x2c), 1), wc)
         yg = M.PwConvFn.apply(xg, x2g, wg)
     else:
@@ -57,7 +58,8 @@ def test_pw_conv(split):
         assert rel_inf(x2g.grad, x2c.grad) <= 1e-4
 
 
-@pytest.mark.parametrize("k,s,hw", [(3, 1, (10, 14)), (5, 1, (9, 12)), (3, 2, (11, 16)), (5, 2, (12, 9))])
+@pytest.mark.parametrize("k,s,hw", [(3, 1, (10, 14)), (5, 1, (9, 12)), (3, 2, (11, 16)), (5, 2, (12, 9)), (5, 1, (3, 4)),
+                                    (3, 2, (2, 3)), (5, 2, (50, 47)), (3, 1, (48, 50))])
 def test_dw_conv(k, s, hw):
     torch.manual_seed(1)
     c = 12
@@ -73,14 +75,17 @@ def test_dw_conv(k, s, hw):
     assert rel_inf(xg.grad, xc.grad) <= 2e-4 and rel_inf(wg.grad, wc.grad) <= 1e-4
 
 
-def test_batchnorm_train():
+@pytest.mark.parametrize("shape,offset", [((3, 16, 7, 5), 0.0), ((2, 6, 70, 71), 5.0)])
+def test_batchnorm_train(shape, offset):
     torch.manual_seed(2)
-    bnc = torch.nn.BatchNorm2d(16)
+    bnc = torch.nn.BatchNorm2d(shape[1])
     bnc.weight.data.uniform_(0.5, 1.5)
     bnc.bias.data.uniform_(-0.2, 0.2)
-    bng = torch.nn.BatchNorm2d(16).cuda()
+    bng = torch.nn.BatchNorm2d(shape[1]).cuda()
     bng.load_state_dict(bnc.state_dict())
-    xc, xg = pair(3, 16, 7, 5, scale=2.0)
+    xc, xg = pair(*shape, scale=2.0)
+    xc.data += offset
+    xg.data += offset
     yc = bnc(xc)
     yg = M.BatchNormTrainFn.apply(xg, bng.weight, bng.bias, bng)
     g = torch.randn_like(yc)
