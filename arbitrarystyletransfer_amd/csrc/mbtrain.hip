@@ -329,9 +329,8 @@ __global__ __launch_bounds__(kT) void bn_part_stats_kernel(const float* __restri
   }
 }
 
-__global__ void bn_finalize_stats_kernel(const float* __restrict__ part, int S, int c, float eps, float momentum,
-                                         float* __restrict__ mean, float* __restrict__ invstd,
-                                         float* __restrict__ run_mean, float* __restrict__ run_var) {
+// per channel: Chan merge of the S segment partials into this process's (count, mean, M2), double
+__global__ void bn_local_stats_kernel(const float* __restrict__ part, int S, int c, double* __restrict__ stats) {
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= c) return;
   const float* p = part + (int64_t)ch * S * 3;
@@ -343,13 +342,37 @@ __global__ void bn_finalize_stats_kernel(const float* __restrict__ part, int S, 
     m2 += m2b + d * d * na * nb / nt;
     na = nt;
   }
-  const double var = m2 / na;
+  stats[3 * ch] = na;
+  stats[3 * ch + 1] = mu;
+  stats[3 * ch + 2] = m2;
+}
+
+// merge `parts` processes' [parts][c][3] statistics (SyncBatchNorm: gathered over ranks; 1 part
+// on one GPU) into mean / invstd, the running statistics and 1 / total count
+__global__ void bn_merge_stats_kernel(const double* __restrict__ stats, int parts, int c, float eps, float momentum,
+                                      float* __restrict__ mean, float* __restrict__ invstd,
+                                      float* __restrict__ run_mean, float* __restrict__ run_var,
+                                      float* __restrict__ inv_count) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  double na = 0.0, mu = 0.0, m2 = 0.0;
+  for (int r = 0; r < parts; ++r) {
+    const double* p = stats + ((int64_t)r * c + ch) * 3;
+    const double nb = p[0];
+    if (nb <= 0.0) continue;
+    const double nt = na + nb, d = p[1] - mu;
+    mu += d * nb / nt;
+    m2 += p[2] + d * d * na * nb / nt;
+    na = nt;
+  }
+  const double var = na > 0.0 ? m2 / na : 0.0;
   mean[ch] = (float)mu;
   invstd[ch] = 1.0f / sqrtf((float)var + eps);
   if (run_mean) {
     run_mean[ch] = (1.f - momentum) * run_mean[ch] + momentum * (float)mu;
     run_var[ch] = (1.f - momentum) * run_var[ch] + momentum * (float)(na > 1 ? m2 / (na - 1) : var);
   }
+  if (inv_count && ch == 0) inv_count[0] = (float)(1.0 / na);
 }
 
 // grid (chunks of 4*kT pixels, planes (strided by gridDim.y))
@@ -396,7 +419,7 @@ __global__ __launch_bounds__(kT) void bn_part_bwd_kernel(const float* __restrict
 }
 
 __global__ void bn_finalize_bwd_kernel(const float* __restrict__ part, int S, int c, float* __restrict__ sdy,
-                                       float* __restrict__ sdyx) {
+                                       float* __restrict__ sdyx, float* __restrict__ inv_count, float inv_value) {
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= c) return;
   const float* p = part + (int64_t)ch * S * 2;
@@ -405,12 +428,14 @@ __global__ void bn_finalize_bwd_kernel(const float* __restrict__ part, int S, in
     a += p[2 * i];
     b += p[2 * i + 1];
   }
-  sdy[ch] = (float)a;
-  sdyx[ch] = (float)b;
+  sdy[ch] = (float)a;    // sum dy      (= dbeta)
+  sdyx[ch] = (float)b;   // sum dy xhat (= dgamma)
+  if (inv_count && ch == 0) inv_count[0] = inv_value;
 }
 
 __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                                          int c, int64_t hw, int planes, float inv_m,
+                                                          int c, int64_t hw, int planes,
+                                                          const float* __restrict__ inv_count,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
                                                           const float* __restrict__ gamma,
@@ -419,7 +444,7 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restric
   for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
     const int ch = pl % c;
     const float is = invstd[ch], mu = mean[ch], gm = (gamma ? gamma[ch] : 1.f) * is;
-    const float a = sdy[ch] * inv_m, bq = sdyx[ch] * inv_m;
+    const float inv_m = inv_count[0], a = sdy[ch] * inv_m, bq = sdyx[ch] * inv_m;
     const int64_t base = (int64_t)pl * hw;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -659,41 +684,103 @@ int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, flo
   return (int)hipGetLastError();
 }
 
+// workspace: segment partials (3 floats per (segment, image, channel)), then 8-byte aligned the
+// composite's own [c][3] double statistics and its 1 / count slot
 long long ast_mbt_bn_workspace_floats(int n, int c, long long hw) {
   if (n <= 0 || c <= 0 || hw <= 0) return 0;
-  return 3LL * c * n * ((hw + BN_SEG - 1) / BN_SEG);
+  const long long parts = 3LL * c * n * ((hw + BN_SEG - 1) / BN_SEG);
+  return (parts + 1) / 2 * 2 + 6LL * c + 2;
+}
+
+static int bn_check(int n, int c, long long hw, const float* workspace, long long workspace_floats) {
+  if (!workspace) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hw <= 0 || n > 65535 || c > 65535) return AST_E_SHAPE;
+  if (workspace_floats < ast_mbt_bn_workspace_floats(n, c, hw)) return AST_E_SHAPE;  // workspace too small
+  return 0;
+}
+
+int ast_mbt_bn_stats_f32(const float* x, int n, int c, long long hw, float* workspace, long long workspace_floats,
+                         double* stats, void* stream) {
+  if (!x || !stats) return AST_E_NULLPTR;
+  if (int e = bn_check(n, c, hw, workspace, workspace_floats)) return e;
+  hipStream_t st = (hipStream_t)stream;
+  const int segs = (int)((hw + BN_SEG - 1) / BN_SEG);
+  hipLaunchKernelGGL(bn_part_stats_kernel, dim3(segs, n, c), dim3(kT), 0, st, x, c, (int64_t)hw, workspace);
+  hipLaunchKernelGGL(bn_local_stats_kernel, dim3((c + 63) / 64), dim3(64), 0, st, workspace, segs * n, c, stats);
+  return (int)hipGetLastError();
+}
+
+int ast_mbt_bn_merge_f32(const double* stats, int parts, int c, float eps, float momentum, float* mean, float* invstd,
+                         float* run_mean, float* run_var, float* inv_count, void* stream) {
+  if (!stats || !mean || !invstd || ((run_mean == nullptr) != (run_var == nullptr))) return AST_E_NULLPTR;
+  if (parts <= 0 || c <= 0) return AST_E_SHAPE;
+  hipLaunchKernelGGL(bn_merge_stats_kernel, dim3((c + 63) / 64), dim3(64), 0, (hipStream_t)stream, stats, parts, c,
+                     eps, momentum, mean, invstd, run_mean, run_var, inv_count);
+  return (int)hipGetLastError();
+}
+
+int ast_mbt_bn_apply_f32(const float* x, int n, int c, long long hw, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, float* y, void* stream) {
+  if (!x || !mean || !invstd || !y) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hw <= 0 || (int64_t)n * c > 0x7fffffffLL) return AST_E_SHAPE;
+  hipLaunchKernelGGL(bn_apply_kernel, plane_grid(hw, (int64_t)n * c), dim3(kT), 0, (hipStream_t)stream, x, c,
+                     (int64_t)hw, n * c, mean, invstd, gamma, beta, y);
+  return (int)hipGetLastError();
 }
 
 int ast_mbt_bn_fwd_f32(const float* x, int n, int c, long long hw, const float* gamma, const float* beta, float eps,
                        float momentum, float* mean, float* invstd, float* run_mean, float* run_var, float* y,
                        float* workspace, long long workspace_floats, void* stream) {
-  if (!x || !mean || !invstd || !y || !workspace) return AST_E_NULLPTR;
-  if (n <= 0 || c <= 0 || hw <= 0 || n > 65535 || c > 65535) return AST_E_SHAPE;
-  if (workspace_floats < ast_mbt_bn_workspace_floats(n, c, hw)) return AST_E_SHAPE;  // workspace too small
+  if (!x || !mean || !invstd || !y) return AST_E_NULLPTR;
+  if (int e = bn_check(n, c, hw, workspace, workspace_floats)) return e;
+  const long long off = ast_mbt_bn_workspace_floats(n, c, hw) - 6LL * c - 2;
+  double* stats = (double*)(workspace + off);
+  int e = ast_mbt_bn_stats_f32(x, n, c, hw, workspace, workspace_floats, stats, stream);
+  if (!e) e = ast_mbt_bn_merge_f32(stats, 1, c, eps, momentum, mean, invstd, run_mean, run_var, nullptr, stream);
+  if (!e) e = ast_mbt_bn_apply_f32(x, n, c, hw, mean, invstd, gamma, beta, y, stream);
+  return e;
+}
+
+int ast_mbt_bn_bwd_sums_f32(const float* x, const float* dy, int n, int c, long long hw, const float* mean,
+                            const float* invstd, float* workspace, long long workspace_floats, float* sums,
+                            void* stream) {
+  if (!x || !dy || !mean || !invstd || !sums) return AST_E_NULLPTR;
+  if (int e = bn_check(n, c, hw, workspace, workspace_floats)) return e;
   hipStream_t st = (hipStream_t)stream;
   const int segs = (int)((hw + BN_SEG - 1) / BN_SEG);
-  hipLaunchKernelGGL(bn_part_stats_kernel, dim3(segs, n, c), dim3(kT), 0, st, x, c, (int64_t)hw, workspace);
-  hipLaunchKernelGGL(bn_finalize_stats_kernel, dim3((c + 63) / 64), dim3(64), 0, st, workspace, segs * n, c, eps,
-                     momentum, mean, invstd, run_mean, run_var);
-  hipLaunchKernelGGL(bn_apply_kernel, plane_grid(hw, (int64_t)n * c), dim3(kT), 0, st, x, c, (int64_t)hw, n * c, mean,
-                     invstd, gamma, beta, y);
+  hipLaunchKernelGGL(bn_part_bwd_kernel, dim3(segs, n, c), dim3(kT), 0, st, x, dy, c, (int64_t)hw, mean, invstd,
+                     workspace);
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((c + 63) / 64), dim3(64), 0, st, workspace, segs * n, c, sums,
+                     sums + c, nullptr, 0.f);
+  return (int)hipGetLastError();
+}
+
+int ast_mbt_bn_bwd_apply_f32(const float* x, const float* dy, int n, int c, long long hw, const float* mean,
+                             const float* invstd, const float* gamma, const float* sums, const float* inv_count,
+                             float* dx, void* stream) {
+  if (!x || !dy || !mean || !invstd || !sums || !inv_count || !dx) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hw <= 0 || (int64_t)n * c > 0x7fffffffLL) return AST_E_SHAPE;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, plane_grid(hw, (int64_t)n * c), dim3(kT), 0, (hipStream_t)stream, x, dy, c,
+                     (int64_t)hw, n * c, inv_count, mean, invstd, gamma, sums, sums + c, dx);
   return (int)hipGetLastError();
 }
 
 int ast_mbt_bn_bwd_f32(const float* x, const float* dy, int n, int c, long long hw, const float* mean,
                        const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dx,
                        float* workspace, long long workspace_floats, void* stream) {
-  if (!x || !dy || !mean || !invstd || !dgamma || !dbeta || !dx || !workspace) return AST_E_NULLPTR;
-  if (n <= 0 || c <= 0 || hw <= 0 || n > 65535 || c > 65535) return AST_E_SHAPE;
-  if (workspace_floats < ast_mbt_bn_workspace_floats(n, c, hw)) return AST_E_SHAPE;  // workspace too small
+  if (!dgamma || !dbeta) return AST_E_NULLPTR;
+  if (int e = bn_check(n, c, hw, workspace, workspace_floats)) return e;
+  if (!x || !dy || !mean || !invstd || !dx) return AST_E_NULLPTR;
+  const long long off = ast_mbt_bn_workspace_floats(n, c, hw) - 6LL * c - 2;
+  float* inv_count = workspace + off;
   hipStream_t st = (hipStream_t)stream;
   const int segs = (int)((hw + BN_SEG - 1) / BN_SEG);
   hipLaunchKernelGGL(bn_part_bwd_kernel, dim3(segs, n, c), dim3(kT), 0, st, x, dy, c, (int64_t)hw, mean, invstd,
                      workspace);
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((c + 63) / 64), dim3(64), 0, st, workspace, segs * n, c, dbeta,
-                     dgamma);
+                     dgamma, inv_count, (float)(1.0 / ((double)n * (double)hw)));
   hipLaunchKernelGGL(bn_bwd_apply_kernel, plane_grid(hw, (int64_t)n * c), dim3(kT), 0, st, x, dy, c, (int64_t)hw,
-                     n * c, 1.0f / (float)((int64_t)n * hw), mean, invstd, gamma, dbeta, dgamma, dx);
+                     n * c, inv_count, mean, invstd, gamma, dbeta, dgamma, dx);
   return (int)hipGetLastError();
 }
 

@@ -77,8 +77,8 @@ class FlatGradArena:
             return
         if dist.get_backend(group) == "nccl":
             dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=group)
-        else:  # gloo (CPU tests) has no AVG
-            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+        else:  # gloo (CPU tests; device tensors staged through the host) has no AVG
+            all_reduce_sum(self.flat, group)
             self.flat.div_(dist.get_world_size(group))
 
     def __call__(self, params=None):
@@ -94,3 +94,55 @@ def broadcast_style_stats(style_mean, style_std, src: int = 0, group=None):
     if dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.broadcast(packed, src=src, group=group)
     return packed[0].view_as(style_mean), packed[1].view_as(style_std)
+
+
+# ------------------------------------------------------------------------------------------------
+# SyncBatchNorm for data-parallel AutoEncoder training: the reference
+# trains with batch statistics over its whole batch (train_autoencoder.py, BatchNorm2d in train
+# mode), so a batch-sharded step must merge the statistics over ranks. Forward: every rank's
+# per-channel (count, mean, M2) in double, [c][3], is all-gathered (W*c*24 bytes) and merged on
+# device (Chan's update); backward: the per-channel sums (dy, dy*xhat) are all-reduced for the
+# input gradient, while dgamma/dbeta stay local (the gradient all-reduce averages them, as DDP).
+# ------------------------------------------------------------------------------------------------
+def convert_sync_batchnorm(module: torch.nn.Module, group=None) -> torch.nn.Module:
+    """Mark every BatchNorm2d of `module` for cross-rank statistics (mbtrain.BatchNormTrainFn);
+    the counterpart of torch.nn.SyncBatchNorm.convert_sync_batchnorm."""
+    for m in module.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m._ast_sync = True
+            m._ast_sync_group = group
+    return module
+
+
+def sync_group(bn):
+    """The process group a BatchNorm syncs over, or None (not marked / not distributed / W = 1)."""
+    if not getattr(bn, "_ast_sync", False) or not dist.is_available() or not dist.is_initialized():
+        return None
+    group = getattr(bn, "_ast_sync_group", None)
+    return None if dist.get_world_size(group) == 1 else (group or dist.group.WORLD)
+
+
+def _staged(t, group):
+    """gloo moves host tensors only: stage a device tensor through the host for it."""
+    return t.cpu() if dist.get_backend(group) == "gloo" and t.device.type != "cpu" else t
+
+
+def all_gather_bn_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
+    """[c][3] double per rank -> [W][c][3] on stats' device."""
+    world = dist.get_world_size(group)
+    src = _staged(stats.contiguous(), group)
+    out = torch.empty((world,) + tuple(stats.shape), dtype=stats.dtype, device=src.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, src, group=group)
+    else:
+        dist.all_gather(list(out.unbind(0)), src, group=group)
+    return out.to(stats.device)
+
+
+def all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place sum over ranks (staged through the host for gloo)."""
+    src = _staged(t, group)
+    dist.all_reduce(src, op=dist.ReduceOp.SUM, group=group)
+    if src is not t:
+        t.copy_(src)
+    return t

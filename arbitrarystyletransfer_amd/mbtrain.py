@@ -13,7 +13,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import dp, ops
 from ._lib import HipOpError, check, lib, ptr, stream_ptr
 
 
@@ -136,7 +136,9 @@ def _bn_workspace(x, n, c, hw):
 
 
 class BatchNormTrainFn(torch.autograd.Function):
-    """BatchNorm2d.forward in training mode (batch statistics; running stats updated in place)."""
+    """BatchNorm2d.forward in training mode (batch statistics; running stats updated in place).
+    A BatchNorm marked by dp.convert_sync_batchnorm takes its statistics over every rank's images
+    (all-gather of per-rank (count, mean, M2), all-reduce of the backward sums)."""
 
     @staticmethod
     def forward(ctx, x, gamma, beta, bn):
@@ -148,26 +150,52 @@ class BatchNormTrainFn(torch.autograd.Function):
         ws = _bn_workspace(x, n, c, h * w)
         track = bn.track_running_stats and bn.running_mean is not None
         momentum = bn.momentum if bn.momentum is not None else 0.1
-        check(lib().ast_mbt_bn_fwd_f32(ptr(x), n, c, h * w, ptr(gamma), ptr(beta), float(bn.eps), float(momentum),
-                                       ptr(mean), ptr(invstd), ptr(bn.running_mean) if track else None,
-                                       ptr(bn.running_var) if track else None, ptr(y), ptr(ws), ws.numel(), _s(x)),
-              "batch norm")
+        rm = ptr(bn.running_mean) if track else None
+        rv = ptr(bn.running_var) if track else None
+        group = dp.sync_group(bn)
+        ctx.group = group
+        inv_count = None
+        if group is None:
+            check(lib().ast_mbt_bn_fwd_f32(ptr(x), n, c, h * w, ptr(gamma), ptr(beta), float(bn.eps), float(momentum),
+                                           ptr(mean), ptr(invstd), rm, rv, ptr(y), ptr(ws), ws.numel(), _s(x)),
+                  "batch norm")
+        else:
+            L = lib()
+            stats = torch.empty((c, 3), device=x.device, dtype=torch.float64)
+            check(L.ast_mbt_bn_stats_f32(ptr(x), n, c, h * w, ptr(ws), ws.numel(), ptr(stats), _s(x)), "bn stats")
+            allst = dp.all_gather_bn_stats(stats, group)
+            inv_count = torch.empty((1,), device=x.device, dtype=torch.float32)
+            check(L.ast_mbt_bn_merge_f32(ptr(allst), allst.shape[0], c, float(bn.eps), float(momentum), ptr(mean),
+                                         ptr(invstd), rm, rv, ptr(inv_count), _s(x)), "bn merge")
+            check(L.ast_mbt_bn_apply_f32(ptr(x), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta), ptr(y),
+                                         _s(x)), "bn apply")
         if track:
             bn.num_batches_tracked.add_(1)   # bookkeeping counter (torch does the same host-side increment)
-        ctx.save_for_backward(x, gamma, mean, invstd)
+        ctx.save_for_backward(x, gamma, mean, invstd, inv_count if inv_count is not None else mean)
         return y
 
     @staticmethod
     def backward(ctx, g):
-        x, gamma, mean, invstd = ctx.saved_tensors
+        x, gamma, mean, invstd, inv_count = ctx.saved_tensors
         g = _f32(g, "grad")
         n, c, h, w = x.shape
         dx = torch.empty_like(x)
-        dgamma = torch.empty_like(mean)
-        dbeta = torch.empty_like(mean)
         ws = _bn_workspace(x, n, c, h * w)
-        check(lib().ast_mbt_bn_bwd_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma), ptr(dgamma),
-                                       ptr(dbeta), ptr(dx), ptr(ws), ws.numel(), _s(g)), "batch norm backward")
+        if ctx.group is None:
+            dgamma = torch.empty_like(mean)
+            dbeta = torch.empty_like(mean)
+            check(lib().ast_mbt_bn_bwd_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma),
+                                           ptr(dgamma), ptr(dbeta), ptr(dx), ptr(ws), ws.numel(), _s(g)),
+                  "batch norm backward")
+            return dx, dgamma, dbeta, None
+        L = lib()
+        sums = torch.empty((2, c), device=x.device, dtype=torch.float32)
+        check(L.ast_mbt_bn_bwd_sums_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(ws), ws.numel(),
+                                        ptr(sums), _s(g)), "bn backward sums")
+        dbeta, dgamma = sums[0].clone(), sums[1].clone()     # local: the gradient all-reduce averages them
+        dp.all_reduce_sum(sums, ctx.group)
+        check(L.ast_mbt_bn_bwd_apply_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma), ptr(sums),
+                                         ptr(inv_count), ptr(dx), _s(g)), "bn backward apply")
         return dx, dgamma, dbeta, None
 
 

@@ -31,7 +31,9 @@ import json
 import os
 
 import torch
+import torch.distributed as dist
 
+from . import dp
 from . import losses as L
 from . import models
 from .optim import FusedAdam
@@ -175,6 +177,12 @@ class AutoencoderTrainer:
         self.pretrained_mobnet.requires_grad_(False)
         self.ae_optim = FusedAdam(list(self.model.parameters()), lr=self.args.lr, betas=(0.9, 0.99), eps=1e-7,
                                   max_grad_norm=10.0)
+        # data-parallel (one process per GPU, batch-sharded): SyncBatchNorm keeps the reference's
+        # whole-batch statistics, one all-reduce averages the gradient arena before clip + Adam
+        self.grad_arena = None
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dp.convert_sync_batchnorm(self.model)
+            self.grad_arena = dp.FlatGradArena(list(self.model.parameters()))
         self.save_file = os.path.join(self.args.save_dir, "ae.pth")
         self.train_dict_file = os.path.join(self.args.save_dir, "train_dict.json")
         self.train_dict = {"train_loss": [], "val_loss": [], "perp_loss": []}
@@ -194,6 +202,8 @@ class AutoencoderTrainer:
         out = self.compute_losses(content_imgs)
         self.ae_optim.zero_grad(set_to_none=True)
         out["loss"].backward()
+        if self.grad_arena is not None:
+            self.grad_arena.all_reduce()
         self.ae_optim.step()                                                           # clip 10 + Adam, :159-165
         out["grad_norm"] = self.ae_optim.last_grad_norm
         if record:

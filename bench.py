@@ -120,8 +120,9 @@ def ae_train_bench(args, dev, rank, world):
     """AutoEncoder training step (train_autoencoder.py:124-165): the MobileNet
     AutoEncoder in training mode (BatchNorm batch statistics), reconstruction + perceptual Huber
     losses through the frozen VGG loss network, backward, clip 10 + Adam. bs=16 at 160x160 (the
-    reference's batch size and its largest training size, conf.py img_sizes). N > 1: each rank
-    steps its own replica on its own batch (replicas only; the reference trains on one GPU)."""
+    reference's batch size and its largest training size, conf.py img_sizes). N > 1: data parallel,
+    bs=16 per rank (weak scaling), SyncBatchNorm (all-gather of per-rank BN statistics, all-reduce
+    of the backward sums) and one gradient all-reduce over RCCL before clip + Adam."""
     from arbitrarystyletransfer_amd.train import AutoencoderTrainer, default_ae_args
     B, S = args.batch or 16, args.size or 160
     trainer = AutoencoderTrainer(default_ae_args(batch_size=B), device=dev,
@@ -162,7 +163,8 @@ def ae_train_bench(args, dev, rank, world):
         "data": "synthetic (live-init weights, U[0,1) images), resident in HBM",
         "config": {"workload": f"AutoEncoder train step (MobileNet encoder/decoder, BatchNorm train mode; recon + "
                                f"perceptual Huber via VGG relu_1..relu_15; clip 10 + Adam), bs={B}/GPU {S}x{S} fp32",
-                   "global_batch": B * world, "image_size": S, "parallelism": f"replicas x{world}"},
+                   "global_batch": B * world, "image_size": S,
+                   "parallelism": f"data-parallel x{world}" + (" + SyncBatchNorm" if world > 1 else "")},
         "roofline": {"bound": "mfma", "kernel": "conv3x3 fwd/dgrad + wgrad MFMA launches of a step",
                      "achieved": tf, "peak": PEAK_FP32_MFMA_TF, "unit": "TFLOP/s", "frac": tf / PEAK_FP32_MFMA_TF,
                      "traffic": None, "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3)},

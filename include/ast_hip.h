@@ -384,7 +384,10 @@ int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, flo
 
 /* BatchNorm2d in training mode (batch statistics, biased var + eps; running stats updated with
  * momentum and the unbiased variance when run_mean/run_var are given). mean/invstd [c] saved.
- * workspace: ast_mbt_bn_workspace_floats(n, c, hw) floats of per-segment partial statistics. */
+ * workspace: ast_mbt_bn_workspace_floats(n, c, hw) floats of per-segment partial statistics.
+ * The composites below are stats -> merge(1 part) -> apply and bwd_sums -> bwd_apply; SyncBatchNorm
+ * (data-parallel AutoEncoder training, dp.convert_sync_batchnorm) calls the stages itself with a
+ * gather of the per-rank stats and an all-reduce of the backward sums in between. */
 long long ast_mbt_bn_workspace_floats(int n, int c, long long hw);
 int ast_mbt_bn_fwd_f32(const float* x, int n, int c, long long hw, const float* gamma,
                        const float* beta, float eps, float momentum, float* mean, float* invstd,
@@ -394,6 +397,23 @@ int ast_mbt_bn_bwd_f32(const float* x, const float* dy, int n, int c, long long 
                        const float* mean, const float* invstd, const float* gamma, float* dgamma,
                        float* dbeta, float* dx, float* workspace, long long workspace_floats,
                        void* stream);
+/* this process's per-channel (count, mean, M2) as double [c][3] */
+int ast_mbt_bn_stats_f32(const float* x, int n, int c, long long hw, float* workspace,
+                         long long workspace_floats, double* stats, void* stream);
+/* merge [parts][c][3] stats (Chan) -> mean, invstd, running stats (nullable), 1/count [1] (nullable) */
+int ast_mbt_bn_merge_f32(const double* stats, int parts, int c, float eps, float momentum, float* mean,
+                         float* invstd, float* run_mean, float* run_var, float* inv_count, void* stream);
+int ast_mbt_bn_apply_f32(const float* x, int n, int c, long long hw, const float* mean,
+                         const float* invstd, const float* gamma, const float* beta, float* y,
+                         void* stream);
+/* sums [2][c]: sum(dy), sum(dy * xhat) over this process's images */
+int ast_mbt_bn_bwd_sums_f32(const float* x, const float* dy, int n, int c, long long hw,
+                            const float* mean, const float* invstd, float* workspace,
+                            long long workspace_floats, float* sums, void* stream);
+/* dx from (all-reduced) sums and the device 1/count written by ast_mbt_bn_merge_f32 */
+int ast_mbt_bn_bwd_apply_f32(const float* x, const float* dy, int n, int c, long long hw,
+                             const float* mean, const float* invstd, const float* gamma,
+                             const float* sums, const float* inv_count, float* dx, void* stream);
 
 /* op 0 y = hardswish(a); 1 y = hardswish'(a) * b; 2 y = a + b; 3 y = nearest-upsample x2 of a
  * (n planes of h x w); 4 its backward (a = grad of the 2h x 2w planes). */

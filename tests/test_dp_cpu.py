@@ -111,3 +111,39 @@ def test_style_stats_broadcast_one_style_many_contents(tmp_path):
     got = torch.cat([r0["y"], r1["y"]])
     # CPU convs on different batch sizes pick different algorithms: fp32 reassociation only
     np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=1e-4 * float(np.nanmax(np.abs(ref.numpy()))))
+
+
+def _syncbn_worker(rank, world, port, x, result_path):
+    """SyncBatchNorm plumbing (dp.py): per-rank (count, mean, M2) gathered over gloo and merged
+    (oracle Chan merge) equal the whole batch's statistics; the backward sums all-reduce."""
+    from oracle import ref_cpu as R
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a, b = dp.shard_range(x.shape[0], rank, world)
+    local = torch.from_numpy(R.bn_shard_stats(x[a:b].numpy()))
+    allst = dp.all_gather_bn_stats(local)
+    sums = torch.tensor([[float(rank + 1)] * 3, [2.0 * (rank + 1)] * 3])
+    dp.all_reduce_sum(sums)
+    bn = torch.nn.BatchNorm2d(3)
+    assert dp.sync_group(bn) is None
+    dp.convert_sync_batchnorm(torch.nn.Sequential(bn))
+    assert dp.sync_group(bn) is not None
+    torch.save({"allst": allst, "sums": sums}, result_path + f".{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_syncbn_stats_gather_and_merge(tmp_path):
+    from oracle import ref_cpu as R
+    x = torch.from_numpy(synth.image(931, (5, 3, 7, 6))) * 3 + 2   # ragged shards: 3 + 2 images
+    path = str(tmp_path / "bn")
+    mp.spawn(_syncbn_worker, args=(2, _free_port(), x, path), nprocs=2, join=True)
+    r0 = torch.load(path + ".0", weights_only=True)
+    r1 = torch.load(path + ".1", weights_only=True)
+    assert torch.equal(r0["allst"], r1["allst"]) and r0["allst"].shape == (2, 3, 3)
+    mu, var, cnt = R.bn_merge_stats(r0["allst"].numpy())
+    xn = x.numpy().astype(np.float64)
+    np.testing.assert_allclose(mu, xn.mean(axis=(0, 2, 3)), rtol=1e-12)
+    np.testing.assert_allclose(var, xn.var(axis=(0, 2, 3)), rtol=1e-10)
+    assert (cnt == 5 * 7 * 6).all()
+    assert torch.equal(r0["sums"], torch.tensor([[3.0] * 3, [6.0] * 3])) and torch.equal(r0["sums"], r1["sums"])

@@ -227,3 +227,45 @@ def test_autoencoder_train_step_golden():
         if f"buf:{n}" in g.files:
             assert rel_inf(b, g[f"buf:{n}"]) <= 1e-4, n
     print(f"grad worst {worst:.2e} ({sorted(rows)[-1][2]}); params off by > 1e-6: {far}/{total}")
+
+
+def test_autoencoder_dp_syncbn_step_golden(tmp_path):
+    """Two ranks (torch.distributed.run, gloo on the one GPU), one image each, SyncBatchNorm and
+    the averaged gradient arena: the step equals the reference's single-process step on both
+    images (train_autoencoder.py; SURVEY.md §8f next #4)."""
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "dp.npz")
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "ae_dp_worker.py")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", worker, out],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    got = np.load(out)
+    g = np.load(GOLDEN)
+    for i, k in enumerate(("recon_loss", "content_loss", "loss")):
+        np.testing.assert_allclose(got["losses"][i], float(g[k]), rtol=1e-4, err_msg=k)
+    assert rel_inf(got["recon"], g["recon"]) <= 1e-4
+    norm = float(got["grad_norm"])
+    np.testing.assert_allclose(norm, float(g["grad_norm"]), rtol=1e-3)
+    worst = 0.0
+    for key in g.files:
+        if not key.startswith("grad:"):
+            continue
+        ref = g[key]
+        mine = got[key].reshape(-1)
+        mine = (mine if mine.size == ref.size else mine[::17]).reshape(ref.shape)
+        worst = max(worst, float(np.abs(mine - ref).max()) / max(float(np.abs(ref).max()), 1e-5 * norm))
+        pref = g["param:" + key[5:]]
+        pv = got["param:" + key[5:]].reshape(-1)
+        pv = (pv if pv.size == pref.size else pv[::17]).reshape(pref.shape)
+        assert np.abs(pv - pref).max() <= 2.05 * 2e-4, key
+    assert worst <= 1e-3, worst
+    for key in g.files:
+        if key.startswith("buf:"):
+            assert rel_inf(got[key], g[key]) <= 1e-4, key
