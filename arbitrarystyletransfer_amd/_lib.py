@@ -75,6 +75,8 @@ SIGNATURES = {
     "ast_aug_resize_workspace_floats": (ctypes.c_size_t, [_i, _i, _i]),
     "ast_aug_resize_f32": (_i, [_p, _i, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _p]),
     "ast_aug_blur_f32": (_i, [_p, _i, _i, _i, _p, _i, _p, _p, _p]),
+    "ast_pack_images_f32": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _i, _p, _p]),
+    "ast_unpack_images_f32": (_i, [_p, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
     "ast_mbt_gemm_f32": (_i, [_p, _p, _p, _i, _i, _i, _i, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _i, _i, _i, _i, _i,
                               _p]),
     "ast_mbt_dw_f32": (_i, [_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),

@@ -30,6 +30,7 @@ DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1}
 # When a list, every block forward appends its block-fused minimum HBM bytes (read the block input
 # once, write its output once) — bench.py's config-5 roofline denominator.
 IO_TRACE = None
+DW_TRACE = None   # bench.py: per expand_dw launch, the depthwise multiply-adds (VALU work)
 
 
 def _trace_io(nbytes: int) -> None:
@@ -296,6 +297,8 @@ class DepthWiseConv(nn.Module):
               "DepthWiseConv SE")
         out = torch.empty((n, cout, ho, wo), device=dev, dtype=dt)
         _trace_io(es * (n * cin * h * w + out.numel()))
+        if DW_TRACE is not None:   # depthwise FMAs of the expand_dw launch (bench.py's VALU figure)
+            DW_TRACE.append(n * hid * ho * wo * k * k)
         res = x if self.identity else None
         nb2 = es * (d.numel() + out.numel() + (res.numel() if res is not None else 0))
         check(ops._timed(f"mb pw {hid}->{cout} {ho}x{wo}", -nb2, dev, lambda: lib().ast_mb_pw(

@@ -7,6 +7,8 @@ into a hipGraph. CPU tensors raise: there is no CPU fallback in the product path
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._lib import HipOpError, check, lib, ptr, stream_ptr
@@ -102,10 +104,26 @@ def pack_conv3x3(weight: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def pack_plan(n: int, w: int, pool: bool):
+    """(G, gap) for side-by-side packing of n planes of width w (csrc/pack.hip): the group size
+    that best fills the conv kernel's 32-pixel MFMA row tiles, if it gains >= 15%; (1, 0) else."""
+    if os.environ.get("AST_CONV_PACK", "1") == "0" or n < 2 or w > 64 or (pool and w % 2):
+        return 1, 0
+    gap = 2 if pool else 1
+    base = w / (-(-w // 32) * 32)
+    best_u, best_g = base, 1
+    for g in range(2, min(n, 8) + 1):
+        wp = g * (w + gap) - gap
+        u = n * w / (-(-n // g) * (-(-wp // 32) * 32))
+        if u > best_u * 1.0001:
+            best_u, best_g = u, g
+    return (best_g, gap) if best_u >= 1.15 * base else (1, 0)
+
+
 def conv3x3(x: torch.Tensor, w_packed: torch.Tensor, bias, cout: int, *, upsample: int = 1,
             pad_mode: str = "zeros", in_mean=None, in_std=None,
             want_pre: bool = False, want_act: bool = True, want_pool: bool = False, cfg: int = -1,
-            x2: torch.Tensor | None = None):
+            x2: torch.Tensor | None = None, _pack: bool = True, _flops=None):
     """Fused [Upsample x2] -> pad(1) -> Conv3x3 -> (+bias) -> {pre, ReLU, ReLU+MaxPool2x2}.
 
     x2 (optional): a second batch with x's C, H, W; outputs hold x's images then x2's (one
@@ -148,7 +166,25 @@ def conv3x3(x: torch.Tensor, w_packed: torch.Tensor, bias, cout: int, *, upsampl
         raise HipOpError("conv3x3: no output requested")
     if cfg < 0:
         cfg = tuned_config(n, cin, h_in, w_in, cout, upsample, pad_mode, want_pool)
-    flops = 2 * n * H * W * cout * cin * 9
+    G, gap = pack_plan(n, w_in, want_pool) if (_pack and pad_mode == "zeros" and upsample == 1
+                                                and in_mean is None) else (1, 0)
+    if G > 1:   # small planes: G images side by side per row band (identical results, fuller tiles)
+        L = lib()
+        ng, wp = -(-n // G), G * (w_in + gap) - gap
+        xp = torch.empty((ng, cin, h_in, wp), device=x.device, dtype=torch.float32)
+        check(L.ast_pack_images_f32(ptr(x), n1, ptr(x2), n2, cin, h_in, w_in, G, gap, ptr(xp),
+                                    stream_ptr(x.device)), "pack")
+        outs = conv3x3(xp, w_packed, bias, cout, want_pre=want_pre, want_act=want_act, want_pool=want_pool,
+                       cfg=cfg, _pack=False, _flops=2 * n * H * W * cout * cin * 9)
+        res = []
+        for t, full, hh, ww in ((outs[0], pre, H, W), (outs[1], act, H, W), (outs[2], pool, H // 2, W // 2)):
+            if t is not None:
+                sp, wpp = (w_in + gap, wp) if hh == H else ((w_in + gap) // 2, wp // 2)
+                check(L.ast_unpack_images_f32(ptr(t), n, cout, hh, ww, G, sp, wpp, ptr(full), stream_ptr(x.device)),
+                      "unpack")
+            res.append(full if t is not None else None)
+        return tuple(res)
+    flops = _flops if _flops is not None else 2 * n * H * W * cout * cin * 9
     tag = f"conv3x3 {cin}->{cout} {H}x{W} up{upsample} {pad_mode}"
     code = _timed(tag, flops, x.device, lambda: lib().ast_conv3x3_fwd_f32_cfg(
         cfg, ptr(x), ptr(x2), n2, ptr(w_packed), ptr(bias), ptr(pre), ptr(act), ptr(pool), ptr(in_mean),

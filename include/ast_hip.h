@@ -367,6 +367,14 @@ int ast_aug_blur_f32(const float* src, int c, int h, int w, const float* taps, i
  * fp32, composable kernels with their backward (csrc/mbtrain.hip).
  * ------------------------------------------------------------------------------------------ */
 
+/* Side-by-side packing for small-plane zero-padded 3x3 convs (csrc/pack.hip; ops.conv3x3):
+ * xp[ceil(n/G)][c][h][G*(w+gap)-gap] holds images x[0..n1) then x2[0..n2), G per row band,
+ * `gap` zero columns between them; unpack reads image i at column (i%G)*sp of packed plane i/G. */
+int ast_pack_images_f32(const float* x, int n1, const float* x2, int n2, int c, int h, int w, int G,
+                        int gap, float* xp, void* stream);
+int ast_unpack_images_f32(const float* yp, int n, int c, int h, int w, int G, int sp, int wp,
+                          float* out, void* stream);
+
 /* C[b][m][n] (+)= sum_k A[b][m][k] B[b][k][n] with element strides (1x1 convs and their grads).
  * ksplit > 1 splits K across workgroups; partial sums are then atomically added (as when C is
  * shared across the batch, sCb == 0): C must hold the starting value (zero it to overwrite).
