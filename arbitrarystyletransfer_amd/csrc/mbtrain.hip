@@ -174,73 +174,92 @@ __device__ __forceinline__ int refl(int i, int n) {
   return i >= n ? 2 * (n - 1) - i : i;
 }
 
+// grid (pixel chunks of kT, planes strided by gridDim.y): the plane, hence the channel and its
+// K*K weights, is uniform per workgroup (scalar loads)
 template <int K, int S>
 __global__ __launch_bounds__(kT) void dw_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                    float* __restrict__ y, int total, int c, int h, int wd, int ho,
+                                                    float* __restrict__ y, int planes, int c, int h, int wd, int ho,
                                                     int wo) {
   constexpr int P = (K - 1) / 2;
   const int e = blockIdx.x * kT + threadIdx.x;
-  if (e >= total) return;
   const int hwo = ho * wo;
-  const int pl = e / hwo, rem = e - pl * hwo;
-  const int oy = rem / wo, ox = rem - oy * wo;
-  const float* xp = x + (int64_t)pl * h * wd;
-  const float* wc = w + (pl % c) * K * K;
+  const int oy = e / wo, ox = e - oy * wo;
   int ix[K];
 #pragma unroll
   for (int kx = 0; kx < K; ++kx) ix[kx] = refl(ox * S - P + kx, wd);
-  float acc = 0.f;
+  for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
+    const float* wc = w + (pl % c) * K * K;
+    float wr[K * K];
 #pragma unroll
-  for (int ky = 0; ky < K; ++ky) {
-    const float* row = xp + refl(oy * S - P + ky, h) * wd;
+    for (int t = 0; t < K * K; ++t) wr[t] = wc[t];
+    if (e >= hwo) continue;
+    const float* xp = x + (int64_t)pl * h * wd;
+    float acc = 0.f;
 #pragma unroll
-    for (int kx = 0; kx < K; ++kx) acc = fmaf(wc[ky * K + kx], row[ix[kx]], acc);
+    for (int ky = 0; ky < K; ++ky) {
+      const float* row = xp + refl(oy * S - P + ky, h) * wd;
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) acc = fmaf(wr[ky * K + kx], row[ix[kx]], acc);
+    }
+    y[(int64_t)pl * hwo + e] = acc;
   }
-  y[e] = acc;
 }
 
 // dx[i][j] = sum over the padded positions q that reflect onto (i, j) and the taps t with
 // (q - t) = s * o for an output o of g[o] * w[t] -- a gather, no atomics. Per axis an input index
 // i has the interior preimage q = i + p, a top-pad preimage p - i (1 <= i <= p) and a bottom-pad
-// preimage 2(n-1) - i + p (n-1-p <= i <= n-2).
+// preimage 2(n-1) - i + p (n-1-p <= i <= n-2). Grid as dw_fwd_kernel, over input pixels.
 template <int K, int S>
 __global__ __launch_bounds__(kT) void dw_dgrad_kernel(const float* __restrict__ g, const float* __restrict__ w,
-                                                      float* __restrict__ dx, int total, int c, int h, int wd, int ho,
+                                                      float* __restrict__ dx, int planes, int c, int h, int wd, int ho,
                                                       int wo) {
   constexpr int P = (K - 1) / 2;
   const int e = blockIdx.x * kT + threadIdx.x;
-  if (e >= total) return;
   const int hw = h * wd;
-  const int pl = e / hw, rem = e - pl * hw;
-  const int iy = rem / wd, ix = rem - iy * wd;
-  const float* gp = g + (int64_t)pl * ho * wo;
-  const float* wc = w + (pl % c) * K * K;
-  float acc = 0.f;
+  const int iy = e / wd, ix = e - iy * wd;
+  for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
+    const float* wc = w + (pl % c) * K * K;
+    float wr[K * K];
 #pragma unroll
-  for (int ry = 0; ry < 3; ++ry) {
-    const bool vy = ry == 0 || (ry == 1 && iy >= 1 && iy <= P) || (ry == 2 && iy >= h - 1 - P && iy <= h - 2);
-    if (!vy) continue;
-    const int qy = ry == 0 ? iy + P : (ry == 1 ? P - iy : 2 * (h - 1) - iy + P);
+    for (int t = 0; t < K * K; ++t) wr[t] = wc[t];
+    if (e >= hw) continue;
+    const float* gp = g + (int64_t)pl * ho * wo;
+    float acc = 0.f;
+    if (S == 1 && iy > P && iy < h - 1 - P && ix > P && ix < wd - 1 - P) {  // interior: one preimage, all taps
+      const float* gc = gp + (iy + P) * wo + ix + P;
 #pragma unroll
-    for (int ty = 0; ty < K; ++ty) {
-      const int t = qy - ty;
-      if (t < 0 || (t % S) != 0 || t / S >= ho) continue;
-      const float* grow = gp + (t / S) * wo;
+      for (int ty = 0; ty < K; ++ty)
 #pragma unroll
-      for (int rx = 0; rx < 3; ++rx) {
-        const bool vx = rx == 0 || (rx == 1 && ix >= 1 && ix <= P) || (rx == 2 && ix >= wd - 1 - P && ix <= wd - 2);
-        if (!vx) continue;
-        const int qx = rx == 0 ? ix + P : (rx == 1 ? P - ix : 2 * (wd - 1) - ix + P);
+        for (int tx = 0; tx < K; ++tx) acc = fmaf(gc[-ty * wo - tx], wr[ty * K + tx], acc);
+      dx[(int64_t)pl * hw + e] = acc;
+      continue;
+    }
 #pragma unroll
-        for (int tx = 0; tx < K; ++tx) {
-          const int u = qx - tx;
-          if (u < 0 || (u % S) != 0 || u / S >= wo) continue;
-          acc = fmaf(grow[u / S], wc[ty * K + tx], acc);
+    for (int ry = 0; ry < 3; ++ry) {
+      const bool vy = ry == 0 || (ry == 1 && iy >= 1 && iy <= P) || (ry == 2 && iy >= h - 1 - P && iy <= h - 2);
+      if (!vy) continue;
+      const int qy = ry == 0 ? iy + P : (ry == 1 ? P - iy : 2 * (h - 1) - iy + P);
+#pragma unroll
+      for (int ty = 0; ty < K; ++ty) {
+        const int t = qy - ty;
+        if (t < 0 || (t % S) != 0 || t / S >= ho) continue;
+        const float* grow = gp + (t / S) * wo;
+#pragma unroll
+        for (int rx = 0; rx < 3; ++rx) {
+          const bool vx = rx == 0 || (rx == 1 && ix >= 1 && ix <= P) || (rx == 2 && ix >= wd - 1 - P && ix <= wd - 2);
+          if (!vx) continue;
+          const int qx = rx == 0 ? ix + P : (rx == 1 ? P - ix : 2 * (wd - 1) - ix + P);
+#pragma unroll
+          for (int tx = 0; tx < K; ++tx) {
+            const int u = qx - tx;
+            if (u < 0 || (u % S) != 0 || u / S >= wo) continue;
+            acc = fmaf(grow[u / S], wr[ty * K + tx], acc);
+          }
         }
       }
     }
+    dx[(int64_t)pl * hw + e] = acc;
   }
-  dx[e] = acc;
 }
 
 // dw[c][tap] += sum over a segment of one image's output plane (grid = (segments, n, c)); dw is
@@ -557,6 +576,7 @@ __global__ __launch_bounds__(kT) void se_fc_fwd_kernel(const float* __restrict__
   const float* pv = pool + (int64_t)n * c;
   for (int j = threadIdx.x; j < red; j += kT) {
     float a = b1[j];
+#pragma unroll 16
     for (int i = 0; i < c; ++i) a = fmaf(w1[(int64_t)j * c + i], pv[i], a);
     a = a > 0.f ? a : 0.f;
     hs[j] = a;
@@ -565,6 +585,7 @@ __global__ __launch_bounds__(kT) void se_fc_fwd_kernel(const float* __restrict__
   __syncthreads();
   for (int i = threadIdx.x; i < c; i += kT) {
     float a = b2[i];
+#pragma unroll 16
     for (int j = 0; j < red; ++j) a = fmaf(w2[(int64_t)i * red + j], hs[j], a);
     z[(int64_t)n * c + i] = a;
     gate[(int64_t)n * c + i] = fminf(fmaxf(a, 0.f), 1.f);
@@ -598,6 +619,7 @@ __global__ __launch_bounds__(kT) void se_fc_bwd_kernel(const float* __restrict__
   }
   for (int j = threadIdx.x; j < red; j += kT) {
     float a = 0.f;
+#pragma unroll 16
     for (int i = 0; i < c; ++i) a = fmaf(w2[(int64_t)i * red + j], dz[i], a);
     a = hv[j] > 0.f ? a : 0.f;
     dh[j] = a;
@@ -611,6 +633,7 @@ __global__ __launch_bounds__(kT) void se_fc_bwd_kernel(const float* __restrict__
   }
   for (int i = threadIdx.x; i < c; i += kT) {
     float a = 0.f;
+#pragma unroll 16
     for (int j = 0; j < red; ++j) a = fmaf(w1[(int64_t)j * c + i], dh[j], a);
     dpool[(int64_t)n * c + i] = a * inv_hw;
   }
@@ -669,12 +692,11 @@ int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, flo
   const int64_t nc = (int64_t)n * c;
   if (nc * h * wd >= (1LL << 31) || n > 65535 || c > 65535) return AST_E_SHAPE;  // 32-bit flat indices
   hipStream_t st = (hipStream_t)stream;
+  const unsigned gy = (unsigned)(nc < 65535 ? nc : 65535);
   if (mode == 0) {
-    const int total = (int)(nc * ho * wo);
-    AST_DW_DISPATCH(dw_fwd_kernel, dim3((total + kT - 1) / kT), x, w, out, total, c, h, wd, ho, wo);
+    AST_DW_DISPATCH(dw_fwd_kernel, dim3((ho * wo + kT - 1) / kT, gy), x, w, out, (int)nc, c, h, wd, ho, wo);
   } else if (mode == 1) {
-    const int total = (int)(nc * h * wd);
-    AST_DW_DISPATCH(dw_dgrad_kernel, dim3((total + kT - 1) / kT), g, w, out, total, c, h, wd, ho, wo);
+    AST_DW_DISPATCH(dw_dgrad_kernel, dim3((h * wd + kT - 1) / kT, gy), g, w, out, (int)nc, c, h, wd, ho, wo);
   } else {
     hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)c * k * k, st);
     if (e != hipSuccess) return (int)e;

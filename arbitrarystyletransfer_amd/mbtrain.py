@@ -38,9 +38,10 @@ def gemm(A, B, C, M, N, K, batch, sA, sB, sC, ksplit=1, accumulate=False, fold_k
 
 
 def _ksplit(m, n, k):
-    """Split the weight gradient's long reduction so ~512 workgroups run, chunks >= 512 deep."""
+    """Split the weight gradient's long reduction so ~1024 workgroups run (4 per CU), chunks >= 256
+    deep; the partial tiles meet in C through atomics."""
     tiles = -(-m // 64) * -(-n // 64)
-    return max(1, min(-(-512 // tiles), k // 512))
+    return max(1, min(-(-1024 // tiles), k // 256, 65535))
 
 
 # ------------------------------------------------------------------------------------------------
