@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 TAG="${1:-run}"
 STEPS="${BENCH_STEPS:-10}"
 
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$OUT/${TAG}_tests.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/${TAG}_tests.log" 2>&1
 rc=$?
 echo "gpu tests rc=$rc"; tail -5 "$OUT/${TAG}_tests.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

@@ -246,14 +246,15 @@ def test_config5_shape_bf16_1024(hip_device):
     assert rel_inf(y2[1:], y1) <= 1e-2   # SE pool atomics: order-dependent last bits, then bf16 rounding
 
 
-def test_inference_only_guards(hip_device):
+def test_mode_dispatch_guards(hip_device):
     blk = DepthWiseConv(16, 16, 1, 6, use_norm=True).to(hip_device)
-    x = torch.rand(1, 16, 8, 8, device=hip_device)
-    with pytest.raises(NotImplementedError):
-        with torch.no_grad():
-            blk(x)                      # BatchNorm in training mode
+    x = torch.rand(2, 16, 8, 8, device=hip_device)
+    with torch.no_grad():
+        assert blk(x).shape == (2, 16, 8, 8)   # training mode: the batch-statistics kernels (mbtrain)
+    bns = [m for m in blk.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    assert bns and all(int(m.num_batches_tracked) == 1 for m in bns)
     blk.eval()
     with pytest.raises(NotImplementedError):
-        blk(x)                          # autograd recording
+        blk(x)                          # eval-mode BatchNorm under autograd recording
     with torch.no_grad():
-        assert blk(x).shape == (1, 16, 8, 8)
+        assert blk(x).shape == (2, 16, 8, 8)
