@@ -913,6 +913,61 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
 
   T* out = reinterpret_cast<T*>(a.out) + (int64_t)n * a.cout * hw;
   const T* res = reinterpret_cast<const T*>(a.res);
+  if constexpr (BF) {
+    // Whole tile, no upsampled residual: the accumulators go through LDS (16 output channels at a
+    // time, fp32, row pitch 260 floats: conflict-free) so every lane stores 8 consecutive pixels
+    // with one 16-byte write (the direct epilogue's 2-byte stores cover 32-byte runs only).
+    constexpr int EP = kPwPx + 4;
+    static_assert(16 * EP * sizeof(float) <= sizeof(ds), "epilogue staging fits the D image");
+    if (vec && (hw % 8) == 0 && (!a.res_up || (a.w % 8) == 0)) {
+      float* st = reinterpret_cast<float*>(ds);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        if (m * 16 >= a.cout) break;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) st[(4 * (lane >> 4) + r) * EP + wave * 64 + t * 16 + (lane & 15)] = acc[m][t][r];
+        lds_barrier();
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int e = tid + i * kThreads, row = e >> 5, q = (e & 31) * 8;  // 16 rows x 32 vectors
+          const int co = m * 16 + row;
+          if (co < a.cout) {
+            const f32x4 v0 = *reinterpret_cast<const f32x4*>(st + row * EP + q);
+            const f32x4 v1 = *reinterpret_cast<const f32x4*>(st + row * EP + q + 4);
+            const float bco = a.bias ? a.bias[co] : 0.f;
+            float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+            const int64_t off = (int64_t)co * hw + p0 + q;
+            if (res && a.res_up) {  // nearest x2 residual: 4 source pixels, each used twice
+              const int pix = (int)(p0 + q), y = pix / a.w, x = pix - y * a.w;
+              const int hr = a.h / 2, wr = a.w / 2;
+              const uint2 rv = *reinterpret_cast<const uint2*>(
+                  res + (((int64_t)n * a.cout + co) * hr + (y >> 1)) * wr + (x >> 1));
+              typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+              const bf16x4v rb = __builtin_bit_cast(bf16x4v, rv);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = v[j] + bco + to_f(rb[j >> 1]);
+            } else if (res) {
+              const uint4 rv = *reinterpret_cast<const uint4*>(res + (int64_t)n * a.cout * hw + off);
+              const bf16x8 rb = __builtin_bit_cast(bf16x8, rv);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = v[j] + bco + to_f(rb[j]);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] += bco;
+            }
+            bf16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = from_f<T>(v[j]);
+            *reinterpret_cast<uint4*>(out + off) = __builtin_bit_cast(uint4, o);
+          }
+        }
+        lds_barrier();
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -927,7 +982,7 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
         float v = acc[m][t][r] + bco;
         if (res) {
           if (a.res_up) {
-            const int y = (int)(p / a.w), x = (int)(p % a.w);
+            const int pi = (int)p, y = pi / a.w, x = pi - y * a.w;  // p < h*w < 2^31 (host-checked)
             const int hr = a.h / 2, wr = a.w / 2;
             v += to_f(res[(((int64_t)n * a.cout + co) * hr + (y >> 1)) * wr + (x >> 1)]);
           } else {
@@ -1235,6 +1290,7 @@ int ast_mb_pw(int dtype, const void* d, int n, int hid, int hid_pad, int h, int 
   if (n <= 0 || hid <= 0 || h <= 0 || w <= 0 || cout <= 0) return AST_E_SHAPE;
   if (hid_pad < hid || hid_pad % kPwK != 0 || cout_pad < cout || cout_pad % 16 != 0) return AST_E_SHAPE;
   if (res_up && (h % 2 || w % 2)) return AST_E_SHAPE;
+  if ((int64_t)h * w >= ((int64_t)1 << 31)) return AST_E_SHAPE;  // 32-bit pixel index in the epilogue
   PwArgs a{d, n, hid, hid_pad, h, w, wg, (int64_t)wg_stride, bias, cout, cout_pad, res, res_up ? 1 : 0, out, 0};
   if (dtype == 0) return dispatch_pw<float>(a, (hipStream_t)stream);
   if (dtype == 1) return dispatch_pw<bf16>(a, (hipStream_t)stream);

@@ -49,6 +49,7 @@ BLOCKS = [
     (80, 40, 1, 4, 3, False, True, (1, 16, 16), 1),
     (40, 24, 1, 6, 5, False, True, (1, 64, 64), 1),
     (40, 40, 1, 1, 3, False, True, (1, 9, 13), 2),     # DecoderBlock upsample + ratio-1 block
+    (40, 40, 1, 1, 3, False, True, (2, 16, 24), 2),    # upsample, whole 8-pixel runs (vector pw epilogue)
     (24, 24, 1, 1, 3, False, True, (2, 12, 20), 1),    # ratio-1, no upsample
     (96, 80, 1, 4, 5, False, True, (1, 16, 16), 1),
     (16, 16, 1, 6, 3, False, True, (1, 3, 5), 1),      # tiny map (reflect pad on 3 rows)
