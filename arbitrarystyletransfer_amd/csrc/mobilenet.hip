@@ -173,6 +173,9 @@ __device__ __forceinline__ void store_run(T* o, const float* y, int count) {
   }
 }
 
+#ifndef ED_SKIP
+#define ED_SKIP 0  // experiment builds of the v1 kernel: 1 = no D store, 2 = no depthwise FMAs, 4 = no expand
+#endif
 template <typename T, int K, int S, int UP, bool EXPAND, int TH, int TW>
 __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
   using G = EdGeom<K, S, TH, TW>;
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
     }
     lds_barrier();  // xs (first chunk), ws and the chunk's weights/biases ready
     if (h0 + kChunk < a.hid) ED_FETCH(h0 + kChunk);
-    if (EXPAND) {
+    if (EXPAND && !(ED_SKIP & 4)) {
       float bias[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) bias[r] = b1c[4 * (lane >> 4) + r];
@@ -314,7 +317,7 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
           }
         }
       }
-    } else {
+    } else if (!EXPAND) {
       for (int p = tid; p < G::NP; p += kThreads) {
         const int off = src_off(p);
         float* hp = hs + (p / G::IW) * G::IWP + p % G::IW;
@@ -345,7 +348,7 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
           const int ky = j - r * S;
-          if (ky >= 0 && ky < K) {
+          if (ky >= 0 && ky < K && !(ED_SKIP & 2)) {
 #pragma unroll
             for (int kx = 0; kx < K; ++kx)
 #pragma unroll
@@ -366,7 +369,7 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
             psum += y;
             v[c] = from_f<T>(y);
           }
-          *reinterpret_cast<typename VecOf<T, G::CW>::type*>(drow + r * a.wo) = v;
+          if (!(ED_SKIP & 1)) *reinterpret_cast<typename VecOf<T, G::CW>::type*>(drow + r * a.wo) = v;
         }
       } else {
 #pragma unroll
