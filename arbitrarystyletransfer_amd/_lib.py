@@ -79,7 +79,8 @@ SIGNATURES = {
     "ast_unpack_images_f32": (_i, [_p, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
     "ast_mbt_gemm_f32": (_i, [_p, _p, _p, _i, _i, _i, _i, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _i, _i, _i, _i, _i,
                               _p]),
-    "ast_mbt_dw_f32": (_i, [_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
+    "ast_mbt_dw_workspace_floats": (_ll, [_i, _i, _i, _i, _i]),
+    "ast_mbt_dw_f32": (_i, [_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _ll, _p]),
     "ast_mbt_bn_workspace_floats": (_ll, [_i, _i, _ll]),
     "ast_mbt_bn_fwd_f32": (_i, [_p, _i, _i, _ll, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _ll, _p]),
     "ast_mbt_bn_bwd_f32": (_i, [_p, _p, _i, _i, _ll, _p, _p, _p, _p, _p, _p, _p, _ll, _p]),

@@ -205,60 +205,73 @@ __global__ __launch_bounds__(kT) void dw_fwd_kernel(const float* __restrict__ x,
   }
 }
 
-// dx[i][j] = sum over the padded positions q that reflect onto (i, j) and the taps t with
-// (q - t) = s * o for an output o of g[o] * w[t] -- a gather, no atomics. Per axis an input index
-// i has the interior preimage q = i + p, a top-pad preimage p - i (1 <= i <= p) and a bottom-pad
-// preimage 2(n-1) - i + p (n-1-p <= i <= n-2). Grid as dw_fwd_kernel, over input pixels.
+// Input gradient = reflect_pad^T(conv^T(g)) in two passes, both branch-free in the bulk:
+//  dw_dpad_kernel: the gradient w.r.t. the PADDED input, dpad[q] = sum over taps t with
+//                  (q - t) = s * o for an output o of g[o] * w[t] (invalid taps masked by a zero
+//                  weight and a clamped address, so no lane diverges)
+//  dw_fold_kernel: dx[i] = dpad[i + p] + the pad positions that reflect onto i (per axis: top pad
+//                  p - i for 1 <= i <= p, bottom pad 2(n-1) - i + p for n-1-p <= i <= n-2).
+// Grids as dw_fwd_kernel (pixel chunks x planes).
 template <int K, int S>
-__global__ __launch_bounds__(kT) void dw_dgrad_kernel(const float* __restrict__ g, const float* __restrict__ w,
-                                                      float* __restrict__ dx, int planes, int c, int h, int wd, int ho,
-                                                      int wo) {
-  constexpr int P = (K - 1) / 2;
+__global__ __launch_bounds__(kT) void dw_dpad_kernel(const float* __restrict__ g, const float* __restrict__ w,
+                                                     float* __restrict__ dpad, int planes, int c, int hp, int wp,
+                                                     int ho, int wo) {
   const int e = blockIdx.x * kT + threadIdx.x;
-  const int hw = h * wd;
-  const int iy = e / wd, ix = e - iy * wd;
+  const int qy = e / wp, qx = e - qy * wp;
   for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
     const float* wc = w + (pl % c) * K * K;
     float wr[K * K];
 #pragma unroll
     for (int t = 0; t < K * K; ++t) wr[t] = wc[t];
-    if (e >= hw) continue;
+    if (e >= hp * wp) continue;
     const float* gp = g + (int64_t)pl * ho * wo;
     float acc = 0.f;
-    if (S == 1 && iy > P && iy < h - 1 - P && ix > P && ix < wd - 1 - P) {  // interior: one preimage, all taps
-      const float* gc = gp + (iy + P) * wo + ix + P;
 #pragma unroll
-      for (int ty = 0; ty < K; ++ty)
+    for (int ty = 0; ty < K; ++ty) {
+      const int t = qy - ty;
+      const bool vy = t >= 0 && (t % S) == 0 && t / S < ho;
+      const int oy = min(max(t, 0) / S, ho - 1);
 #pragma unroll
-        for (int tx = 0; tx < K; ++tx) acc = fmaf(gc[-ty * wo - tx], wr[ty * K + tx], acc);
-      dx[(int64_t)pl * hw + e] = acc;
-      continue;
-    }
-#pragma unroll
-    for (int ry = 0; ry < 3; ++ry) {
-      const bool vy = ry == 0 || (ry == 1 && iy >= 1 && iy <= P) || (ry == 2 && iy >= h - 1 - P && iy <= h - 2);
-      if (!vy) continue;
-      const int qy = ry == 0 ? iy + P : (ry == 1 ? P - iy : 2 * (h - 1) - iy + P);
-#pragma unroll
-      for (int ty = 0; ty < K; ++ty) {
-        const int t = qy - ty;
-        if (t < 0 || (t % S) != 0 || t / S >= ho) continue;
-        const float* grow = gp + (t / S) * wo;
-#pragma unroll
-        for (int rx = 0; rx < 3; ++rx) {
-          const bool vx = rx == 0 || (rx == 1 && ix >= 1 && ix <= P) || (rx == 2 && ix >= wd - 1 - P && ix <= wd - 2);
-          if (!vx) continue;
-          const int qx = rx == 0 ? ix + P : (rx == 1 ? P - ix : 2 * (wd - 1) - ix + P);
-#pragma unroll
-          for (int tx = 0; tx < K; ++tx) {
-            const int u = qx - tx;
-            if (u < 0 || (u % S) != 0 || u / S >= wo) continue;
-            acc = fmaf(grow[u / S], wr[ty * K + tx], acc);
-          }
-        }
+      for (int tx = 0; tx < K; ++tx) {
+        const int u = qx - tx;
+        const bool v = vy && u >= 0 && (u % S) == 0 && u / S < wo;
+        const int ox = min(max(u, 0) / S, wo - 1);
+        acc = fmaf(gp[oy * wo + ox], v ? wr[ty * K + tx] : 0.f, acc);
       }
     }
-    dx[(int64_t)pl * hw + e] = acc;
+    dpad[(int64_t)pl * hp * wp + e] = acc;
+  }
+}
+
+template <int P>
+__global__ __launch_bounds__(kT) void dw_fold_kernel(const float* __restrict__ dpad, float* __restrict__ dx, int planes,
+                                                     int h, int wd) {
+  const int hp = h + 2 * P, wp = wd + 2 * P;
+  const int e = blockIdx.x * kT + threadIdx.x;
+  if (e >= h * wd) return;
+  const int iy = e / wd, ix = e - iy * wd;
+  // per axis up to 3 padded preimages; -1 = none
+  const int y1 = (iy >= 1 && iy <= P) ? P - iy : -1;
+  const int y2 = (iy >= h - 1 - P && iy <= h - 2) ? 2 * (h - 1) - iy + P : -1;
+  const int x1 = (ix >= 1 && ix <= P) ? P - ix : -1;
+  const int x2 = (ix >= wd - 1 - P && ix <= wd - 2) ? 2 * (wd - 1) - ix + P : -1;
+  for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
+    const float* d = dpad + (int64_t)pl * hp * wp;
+    const int qy0 = iy + P, qx0 = ix + P;
+    float acc = d[qy0 * wp + qx0];
+    if (x1 >= 0) acc += d[qy0 * wp + x1];
+    if (x2 >= 0) acc += d[qy0 * wp + x2];
+    if (y1 >= 0) {
+      acc += d[y1 * wp + qx0];
+      if (x1 >= 0) acc += d[y1 * wp + x1];
+      if (x2 >= 0) acc += d[y1 * wp + x2];
+    }
+    if (y2 >= 0) {
+      acc += d[y2 * wp + qx0];
+      if (x1 >= 0) acc += d[y2 * wp + x1];
+      if (x2 >= 0) acc += d[y2 * wp + x2];
+    }
+    dx[(int64_t)pl * h * wd + e] = acc;
   }
 }
 
@@ -682,21 +695,34 @@ int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int
     else hipLaunchKernelGGL((KERNEL<5, 2>), grid, dim3(kT), 0, st, __VA_ARGS__);                    \
   } while (0)
 
+long long ast_mbt_dw_workspace_floats(int n, int c, int h, int wd, int k) {
+  if (n <= 0 || c <= 0 || h <= 0 || wd <= 0 || (k != 3 && k != 5)) return 0;
+  return (long long)n * c * (h + k - 1) * (wd + k - 1);
+}
+
 int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, float* out, int n, int c, int h, int wd,
-                   int k, int s, void* stream) {
-  if (!w || !out || (mode != 1 && !x) || (mode != 0 && !g)) return AST_E_NULLPTR;
+                   int k, int s, float* workspace, long long workspace_floats, void* stream) {
+  if (!w || !out || (mode != 1 && !x) || (mode != 0 && !g) || (mode == 1 && !workspace)) return AST_E_NULLPTR;
   if (n <= 0 || c <= 0 || h <= 0 || wd <= 0 || (k != 3 && k != 5) || (s != 1 && s != 2)) return AST_E_SHAPE;
   const int p = (k - 1) / 2;
   if (p >= h || p >= wd) return AST_E_SHAPE;  // reflect padding needs pad < size
   const int ho = (h + 2 * p - k) / s + 1, wo = (wd + 2 * p - k) / s + 1;
   const int64_t nc = (int64_t)n * c;
-  if (nc * h * wd >= (1LL << 31) || n > 65535 || c > 65535) return AST_E_SHAPE;  // 32-bit flat indices
+  if (nc * (h + 2 * p) * (wd + 2 * p) >= (1LL << 31) || n > 65535 || c > 65535) return AST_E_SHAPE;  // 32-bit indices
   hipStream_t st = (hipStream_t)stream;
   const unsigned gy = (unsigned)(nc < 65535 ? nc : 65535);
   if (mode == 0) {
     AST_DW_DISPATCH(dw_fwd_kernel, dim3((ho * wo + kT - 1) / kT, gy), x, w, out, (int)nc, c, h, wd, ho, wo);
   } else if (mode == 1) {
-    AST_DW_DISPATCH(dw_dgrad_kernel, dim3((h * wd + kT - 1) / kT, gy), g, w, out, (int)nc, c, h, wd, ho, wo);
+    if (workspace_floats < ast_mbt_dw_workspace_floats(n, c, h, wd, k)) return AST_E_SHAPE;  // workspace too small
+    const int hp = h + 2 * p, wp = wd + 2 * p;
+    AST_DW_DISPATCH(dw_dpad_kernel, dim3((hp * wp + kT - 1) / kT, gy), g, w, workspace, (int)nc, c, hp, wp, ho, wo);
+    if (p == 1)
+      hipLaunchKernelGGL(dw_fold_kernel<1>, dim3((h * wd + kT - 1) / kT, gy), dim3(kT), 0, st, workspace, out, (int)nc,
+                         h, wd);
+    else
+      hipLaunchKernelGGL(dw_fold_kernel<2>, dim3((h * wd + kT - 1) / kT, gy), dim3(kT), 0, st, workspace, out, (int)nc,
+                         h, wd);
   } else {
     hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)c * k * k, st);
     if (e != hipSuccess) return (int)e;

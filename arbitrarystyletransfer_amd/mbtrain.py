@@ -110,7 +110,7 @@ class DwConvFn(torch.autograd.Function):
         ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
         wt = weight.detach().reshape(c, k * k).contiguous()
         y = torch.empty((n, c, ho, wo), device=x.device, dtype=torch.float32)
-        check(lib().ast_mbt_dw_f32(0, ptr(x), ptr(wt), None, ptr(y), n, c, h, w, k, s, _s(x)), "dw conv")
+        check(lib().ast_mbt_dw_f32(0, ptr(x), ptr(wt), None, ptr(y), n, c, h, w, k, s, None, 0, _s(x)), "dw conv")
         ctx.save_for_backward(x, wt)
         ctx.k, ctx.s, ctx.wshape = k, s, weight.shape
         return y
@@ -123,10 +123,13 @@ class DwConvFn(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            check(lib().ast_mbt_dw_f32(1, None, ptr(wt), ptr(g), ptr(dx), n, c, h, w, ctx.k, ctx.s, _s(g)), "dw dgrad")
+            ws = torch.empty((lib().ast_mbt_dw_workspace_floats(n, c, h, w, ctx.k),), device=x.device,
+                             dtype=torch.float32)
+            check(lib().ast_mbt_dw_f32(1, None, ptr(wt), ptr(g), ptr(dx), n, c, h, w, ctx.k, ctx.s, ptr(ws), ws.numel(),
+                                       _s(g)), "dw dgrad")
         if ctx.needs_input_grad[1]:
             dw = torch.empty((c, ctx.k * ctx.k), device=g.device, dtype=torch.float32)
-            check(lib().ast_mbt_dw_f32(2, ptr(x), ptr(wt), ptr(g), ptr(dw), n, c, h, w, ctx.k, ctx.s, _s(g)),
+            check(lib().ast_mbt_dw_f32(2, ptr(x), ptr(wt), ptr(g), ptr(dw), n, c, h, w, ctx.k, ctx.s, None, 0, _s(g)),
                   "dw wgrad")
             dw = dw.reshape(ctx.wshape)
         return dx, dw, None, None

@@ -386,9 +386,12 @@ int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int
                      int accumulate, int atomic, int foldK, int foldN, void* stream);
 
 /* Depthwise k x k conv (k 3|5, stride 1|2, reflect pad (k-1)/2; mobilenetv2.py:148-149, :116-117):
- * mode 0 out = conv(x, w); 1 out = dx from g (overwritten); 2 out = dw [c][k*k] from x, g. */
+ * mode 0 out = conv(x, w); 1 out = dx from g (overwritten; needs workspace of
+ * ast_mbt_dw_workspace_floats floats: the padded-input gradient); 2 out = dw [c][k*k] from x, g. */
+long long ast_mbt_dw_workspace_floats(int n, int c, int h, int wd, int k);
 int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, float* out, int n,
-                   int c, int h, int wd, int k, int s, void* stream);
+                   int c, int h, int wd, int k, int s, float* workspace, long long workspace_floats,
+                   void* stream);
 
 /* BatchNorm2d in training mode (batch statistics, biased var + eps; running stats updated with
  * momentum and the unbiased variance when run_mean/run_var are given). mean/invstd [c] saved.
