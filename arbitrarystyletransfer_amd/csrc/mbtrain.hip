@@ -218,6 +218,14 @@ __global__ __launch_bounds__(kT) void dw_dpad_kernel(const float* __restrict__ g
                                                      int ho, int wo) {
   const int e = blockIdx.x * kT + threadIdx.x;
   const int qy = e / wp, qx = e - qy * wp;
+  int ox[K];     // clamped source column and 0/1 validity of each column tap (hoisted out of the planes)
+  float mx[K];
+#pragma unroll
+  for (int tx = 0; tx < K; ++tx) {
+    const int u = qx - tx;
+    mx[tx] = (u >= 0 && (u % S) == 0 && u / S < wo) ? 1.f : 0.f;
+    ox[tx] = min(max(u, 0) / S, wo - 1);
+  }
   for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
     const float* wc = w + (pl % c) * K * K;
     float wr[K * K];
@@ -229,15 +237,10 @@ __global__ __launch_bounds__(kT) void dw_dpad_kernel(const float* __restrict__ g
 #pragma unroll
     for (int ty = 0; ty < K; ++ty) {
       const int t = qy - ty;
-      const bool vy = t >= 0 && (t % S) == 0 && t / S < ho;
-      const int oy = min(max(t, 0) / S, ho - 1);
+      const float my = (t >= 0 && (t % S) == 0 && t / S < ho) ? 1.f : 0.f;
+      const float* grow = gp + min(max(t, 0) / S, ho - 1) * wo;
 #pragma unroll
-      for (int tx = 0; tx < K; ++tx) {
-        const int u = qx - tx;
-        const bool v = vy && u >= 0 && (u % S) == 0 && u / S < wo;
-        const int ox = min(max(u, 0) / S, wo - 1);
-        acc = fmaf(gp[oy * wo + ox], v ? wr[ty * K + tx] : 0.f, acc);
-      }
+      for (int tx = 0; tx < K; ++tx) acc = fmaf(grow[ox[tx]], wr[ty * K + tx] * (my * mx[tx]), acc);
     }
     dpad[(int64_t)pl * hp * wp + e] = acc;
   }
