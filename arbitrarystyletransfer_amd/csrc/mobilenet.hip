@@ -1125,9 +1125,17 @@ int launch_ed_th(EdArgs a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+int g_ed_th = 0;  // AST_MB_ED_TH=16|4|2 sets the v1 tile height (A/B measurements)
+
 template <typename T, int K, int S, int UP, bool EXPAND>
 int launch_ed(EdArgs a, hipStream_t st) {
   constexpr int TW = S == 1 ? 32 : 16;  // output tile width; 8/4/2 rows as LDS allows
+  if (g_ed_th == 16 && ed_lds_bytes<T, K, S, 16, TW>(a.cin_pad, EXPAND) <= kLdsBudgetMax)
+    return launch_ed_th<T, K, S, UP, EXPAND, 16, TW>(a, st);
+  if (g_ed_th == 4 && ed_lds_bytes<T, K, S, 4, TW>(a.cin_pad, EXPAND) <= kLdsBudget)
+    return launch_ed_th<T, K, S, UP, EXPAND, 4, TW>(a, st);
+  if (g_ed_th == 2 && ed_lds_bytes<T, K, S, 2, TW>(a.cin_pad, EXPAND) <= kLdsBudget)
+    return launch_ed_th<T, K, S, UP, EXPAND, 2, TW>(a, st);
   if (ed_lds_bytes<T, K, S, 8, TW>(a.cin_pad, EXPAND) <= kLdsBudget)
     return launch_ed_th<T, K, S, UP, EXPAND, 8, TW>(a, st);
   if (ed_lds_bytes<T, K, S, 4, TW>(a.cin_pad, EXPAND) <= kLdsBudget)
@@ -1259,6 +1267,11 @@ int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, i
     return v ? atoi(v) : 1;
   }();
   g_ed_big = big;
+  static const int th = [] {
+    const char* v = getenv("AST_MB_ED_TH");
+    return v ? atoi(v) : 0;
+  }();
+  g_ed_th = th;
   hipError_t e = hipMemsetAsync(pool, 0, sizeof(float) * (size_t)n * hid, st);
   if (e != hipSuccess) return (int)e;
   EdArgs a{x1, x2, c1, n, cin, h, w, h * up, w * up, ho, wo, w1p, b1, hid, expand ? cin_pad : 0, wdw, bdw, d, pool, 0, 0};
