@@ -269,3 +269,39 @@ def test_autoencoder_dp_syncbn_step_golden(tmp_path):
     for key in g.files:
         if key.startswith("buf:"):
             assert rel_inf(got[key], g[key]) <= 1e-4, key
+
+
+def test_autoencoder_trainer_loop_checkpoint(tmp_path):
+    """AutoencoderTrainer.train / validate / save / load (train_autoencoder.py:88-120): the loop
+    records the reference's train_dict keys, ae.pth holds {"AE", "optim"}, and a reloaded trainer
+    continues identically (up to float-atomic summation order)."""
+    from arbitrarystyletransfer_amd.train import AutoencoderTrainer, default_ae_args
+    imgs = torch.from_numpy(synth.image(77, (4, 3, 32, 32)))
+
+    def it():
+        while True:
+            yield imgs[:2]
+
+    args = default_ae_args(batch_size=2, train_iter=3, save_dir=str(tmp_path))
+    tr = AutoencoderTrainer(args, content_iter=it(), val_loader=it(), device="cuda",
+                            model=models.AutoEncoder().load_live_init())
+    tr.train()
+    tr.validate()
+    assert len(tr.train_dict["train_loss"]) == 3 and len(tr.train_dict["perp_loss"]) == 3
+    assert len(tr.train_dict["val_loss"]) == 1 and np.isfinite(tr.train_dict["val_loss"][0])
+    assert tr.model.training
+    tr.save()
+    saved = torch.load(os.path.join(str(tmp_path), "ae.pth"), weights_only=True)
+    assert set(saved) == {"AE", "optim"}
+    tr2 = AutoencoderTrainer(args, device="cuda", model=models.AutoEncoder())
+    tr2.load()
+    for (n1, p1), (n2, p2) in zip(tr.model.state_dict().items(), tr2.model.state_dict().items()):
+        assert n1 == n2 and torch.equal(p1, p2), n1
+    x = imgs[2:].cuda()
+    o1 = tr.train_step(x, record=False)
+    o2 = tr2.train_step(x, record=False)
+    # float atomics in the loss and weight-gradient reductions: equal up to summation order
+    np.testing.assert_allclose(o1["loss"].item(), o2["loss"].item(), rtol=1e-6)
+    for p1, p2 in zip(tr.model.parameters(), tr2.model.parameters()):
+        assert float((p1 - p2).detach().abs().max()) <= 2.05 * 2e-4   # Adam steps agree (sign-like first moments)
+        assert rel_inf(p1, p2) <= 1e-3
