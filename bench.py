@@ -175,6 +175,16 @@ def ae_train_bench(args, dev, rank, world):
         print(json.dumps(result), flush=True)
 
 
+def _pmc_traffic(name):
+    """HBM bytes per launch of the dominant kernel, from the committed rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes (profiles/<name>, scripts/pmc_traffic.py); None when absent."""
+    try:
+        with open(os.path.join(ROOT, "profiles", name)) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
 def mobilenet_bench(args, dev, rank, world):
     """Config 5: MobileNet-style variant (Encoder x2 -> AdaIN@[12,14] -> ada_out -> Decoder,
     exporting), bs=32/GPU at 1024x1024, bf16 storage with fp32 arithmetic. The roofline is HBM:
@@ -256,7 +266,10 @@ def mobilenet_bench(args, dev, rank, world):
         # FMAs rather than on HBM: "valu" gives their rate against the 157.3 TF fp32 vector peak.
         "roofline": {"bound": "hbm", "kernel": "mb expand_dw (expand 1x1 MFMA + depthwise kxk VALU, all launches)",
                      "achieved": ed_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": (ed_gbs / PEAK_HBM_GBS) if ed_gbs else None, "traffic": None,
+                     "frac": (ed_gbs / PEAK_HBM_GBS) if ed_gbs else None,
+                     # PMC bytes per expand_dw launch, measured at the default B=32, 1024^2
+                     "traffic": _pmc_traffic("mb_traffic.json") if (B, S) == (32, 1024) and not args.attention
+                     else None,
                      "avg_launch_ms": (ed[1] / ed[2]) if ed else None,
                      "avg_launch_gb": (ed[0] / ed[2] / 1e9) if ed else None,
                      "valu": {"dw_tflops": dw_tf, "peak": PEAK_FP32_MFMA_TF,
@@ -410,14 +423,7 @@ def main():
     adain = [(tag, -fl, ms) for tag, fl, ms in recs if tag.startswith("adain")]
     adain_gbs = (sum(b for _, b, _ in adain) / (sum(m for _, _, m in adain) * 1e-3) / 1e9) if adain else None
 
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "conv_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            with open(tpath) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    traffic = _pmc_traffic("conv_traffic.json")
 
     images = B * world * args.steps
     result = {
