@@ -308,6 +308,107 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgArgs a) {
   if (a.db && cig == 0 && co0 + (tid & 63) < a.Cout) atomicAdd(a.db + co0 + (tid & 63), bacc);
 }
 
+// Weight gradient for Cout <= 4 (the decoders' image convs, models.py:627): as an MFMA GEMM its
+// N = Cout leaves >93% of every 64-wide tile idle, so this is a VALU reduction instead. A workgroup
+// owns SC_CG input channels and sweeps a range of 8x32-pixel tiles (one output pixel per thread):
+// the tile's input halo (padded/upsampled grid coordinates resolved at staging) sits in LDS, each
+// thread accumulates COUT x SC_CG x 9 products of its pixel's dY with the 9 shifted inputs, and
+// the partial dW is reduced over the workgroup (wave shuffles + LDS) into one atomic per weight.
+constexpr int SC_TH = 8, SC_TW = 32, SC_CG = 4, SC_RS = SC_TW + 2, SC_PS = (SC_TH + 2) * SC_RS;
+
+template <int COUT, int UP>
+__global__ __launch_bounds__(256) void wgrad_smallco_kernel(WgArgs a) {
+  __shared__ float xs[SC_CG * SC_PS];
+  __shared__ float red[4][COUT * SC_CG * 9 + COUT];
+  const int Hin = a.Hin, Win = a.Win, H = Hin * UP, W = Win * UP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ty = tid / SC_TW, tx = tid % SC_TW;
+  const int ci_groups = (a.Cin + SC_CG - 1) / SC_CG;
+  const int cig = blockIdx.x % ci_groups;
+  const int64_t split = blockIdx.x / ci_groups;
+  const int ci0 = cig * SC_CG;
+  float acc[COUT][SC_CG * 9];
+  float bacc[COUT];
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) {
+    bacc[o] = 0.f;
+#pragma unroll
+    for (int t = 0; t < SC_CG * 9; ++t) acc[o][t] = 0.f;
+  }
+  const int64_t t0 = a.tiles_per_block * split;
+  const int64_t t1 = min(a.ntiles, t0 + a.tiles_per_block);
+  for (int64_t tile = t0; tile < t1; ++tile) {
+    int64_t tt = tile;
+    const int bx = (int)(tt % a.tiles_x);
+    tt /= a.tiles_x;
+    const int by = (int)(tt % a.tiles_y);
+    const int n = (int)(tt / a.tiles_y);
+    const int x0 = bx * SC_TW, y0 = by * SC_TH;
+    const float* xin = a.x + ((int64_t)n * a.Cin + ci0) * Hin * Win;
+    __syncthreads();
+    for (int e = tid; e < SC_CG * SC_PS; e += 256) {
+      const int c = e / SC_PS, rc = e % SC_PS, r = rc / SC_RS, col = rc % SC_RS;
+      int gy = y0 - 1 + r, gx = x0 - 1 + col;   // padded, upsampled grid
+      float v = 0.f;
+      if (ci0 + c < a.Cin) {
+        bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        if (!ok && a.reflect && gy >= -1 && gy <= H && gx >= -1 && gx <= W) {
+          gy = gy < 0 ? -gy : (gy >= H ? 2 * (H - 1) - gy : gy);
+          gx = gx < 0 ? -gx : (gx >= W ? 2 * (W - 1) - gx : gx);
+          ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        }
+        if (ok) v = xin[((int64_t)c * Hin + gy / UP) * Win + gx / UP];
+      }
+      xs[e] = v;
+    }
+    __syncthreads();
+    const int yy = y0 + ty, xx = x0 + tx;
+    if (yy < H && xx < W) {
+      const float* dyn = a.dy + (int64_t)n * a.Cout * a.dy_plane + a.dy_off + (int64_t)yy * a.dy_pitch + xx;
+      float d[COUT];
+#pragma unroll
+      for (int o = 0; o < COUT; ++o) d[o] = o < a.Cout ? dyn[(int64_t)o * a.dy_plane] : 0.f;
+#pragma unroll
+      for (int o = 0; o < COUT; ++o) bacc[o] += d[o];
+#pragma unroll
+      for (int c = 0; c < SC_CG; ++c)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const float v = xs[c * SC_PS + (ty + ky) * SC_RS + tx + kx];
+#pragma unroll
+            for (int o = 0; o < COUT; ++o) acc[o][c * 9 + ky * 3 + kx] = fmaf(d[o], v, acc[o][c * 9 + ky * 3 + kx]);
+          }
+    }
+  }
+  // reduce over the workgroup: 64-lane shuffles, then the 4 waves through LDS
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) {
+#pragma unroll
+    for (int t = 0; t < SC_CG * 9; ++t) {
+      float v = acc[o][t];
+#pragma unroll
+      for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+      if (lane == 0) red[wave][o * SC_CG * 9 + t] = v;
+    }
+    float b = bacc[o];
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) b += __shfl_xor(b, m, 64);
+    if (lane == 0) red[wave][COUT * SC_CG * 9 + o] = b;
+  }
+  __syncthreads();
+  for (int e = tid; e < COUT * SC_CG * 9 + COUT; e += 256) {
+    const float v = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+    if (e < COUT * SC_CG * 9) {
+      const int o = e / (SC_CG * 9), t = e % (SC_CG * 9), c = t / 9, tap = t % 9;
+      if (o < a.Cout && ci0 + c < a.Cin) atomicAdd(a.dw + ((int64_t)o * a.Cin + ci0 + c) * 9 + tap, v);
+    } else if (a.db && cig == 0 && e - COUT * SC_CG * 9 < a.Cout) {
+      atomicAdd(a.db + (e - COUT * SC_CG * 9), v);
+    }
+  }
+}
+
 // Aligned-shape weight gradient (Cin, Cout multiples of 64; output W a multiple of 32, H even):
 // the same tile, LDS images and MFMA loop as wgrad_kernel, with the staging rebuilt around a
 // register prefetch -- the next tile's input halo (float4 pieces, halo columns as single floats)
@@ -536,6 +637,25 @@ int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* 
   a.x = x; a.dy = dy; a.dw = dw; a.db = db;
   a.N = n; a.Cin = cin; a.Hin = h_in; a.Win = w_in; a.Cout = cout; a.reflect = pad_mode;
   a.dy_pitch = dy_pitch; a.dy_plane = dy_plane; a.dy_off = dy_offset;
+  if (cout <= 4 && !g_wgrad_v1) {  // VALU reduction (wgrad_smallco_kernel)
+    a.tiles_x = cdiv(W, SC_TW);
+    a.tiles_y = cdiv(H, SC_TH);
+    a.ntiles = (int64_t)a.tiles_x * a.tiles_y * n;
+    const int groups = cdiv(cin, SC_CG);
+    int64_t splits = std::max<int64_t>(1, std::min<int64_t>(a.ntiles, (2048 + groups - 1) / groups));
+    a.tiles_per_block = (a.ntiles + splits - 1) / splits;
+    splits = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
+    const int64_t nb = splits * groups;
+    if (nb >= 0x7fffffff) return AST_E_SHAPE;
+    if (cout <= 3) {
+      if (upsample == 2) hipLaunchKernelGGL((wgrad_smallco_kernel<3, 2>), dim3((unsigned)nb), dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((wgrad_smallco_kernel<3, 1>), dim3((unsigned)nb), dim3(256), 0, s, a);
+    } else {
+      if (upsample == 2) hipLaunchKernelGGL((wgrad_smallco_kernel<4, 2>), dim3((unsigned)nb), dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((wgrad_smallco_kernel<4, 1>), dim3((unsigned)nb), dim3(256), 0, s, a);
+    }
+    return (int)hipGetLastError();
+  }
   a.tiles_x = cdiv(W, WG_TW);
   a.tiles_y = cdiv(H, WG_TH);
   a.ntiles = (int64_t)a.tiles_x * a.tiles_y * n;
