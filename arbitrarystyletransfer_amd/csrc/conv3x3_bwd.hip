@@ -308,15 +308,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgArgs a) {
   if (a.db && cig == 0 && co0 + (tid & 63) < a.Cout) atomicAdd(a.db + co0 + (tid & 63), bacc);
 }
 
-// Weight gradient for Cout <= 4 (the decoders' image convs, models.py:627): as an MFMA GEMM its
-// N = Cout leaves >93% of every 64-wide tile idle, so this is a VALU reduction instead. A workgroup
+// Weight gradient for Cout <= 4 (the decoders' image convs, models.py:627), or Cout <= 16 with
+// Cin <= 16 (the MobileNet image convs 3->16 / 16->3): as an MFMA GEMM with 64x64 tiles these
+// leave >93% of every tile idle, so this is a VALU reduction instead. A workgroup
 // owns SC_CG input channels and sweeps a range of 8x32-pixel tiles (one output pixel per thread):
 // the tile's input halo (padded/upsampled grid coordinates resolved at staging) sits in LDS, each
 // thread accumulates COUT x SC_CG x 9 products of its pixel's dY with the 9 shifted inputs, and
 // the partial dW is reduced over the workgroup (wave shuffles + LDS) into one atomic per weight.
-constexpr int SC_TH = 8, SC_TW = 32, SC_CG = 4, SC_RS = SC_TW + 2, SC_PS = (SC_TH + 2) * SC_RS;
+constexpr int SC_TH = 8, SC_TW = 32, SC_RS = SC_TW + 2, SC_PS = (SC_TH + 2) * SC_RS;
 
-template <int COUT, int UP>
+template <int COUT, int SC_CG, int UP>
 __global__ __launch_bounds__(256) void wgrad_smallco_kernel(WgArgs a) {
   __shared__ float xs[SC_CG * SC_PS];
   __shared__ float red[4][COUT * SC_CG * 9 + COUT];
@@ -637,22 +638,27 @@ int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* 
   a.x = x; a.dy = dy; a.dw = dw; a.db = db;
   a.N = n; a.Cin = cin; a.Hin = h_in; a.Win = w_in; a.Cout = cout; a.reflect = pad_mode;
   a.dy_pitch = dy_pitch; a.dy_plane = dy_plane; a.dy_off = dy_offset;
-  if (cout <= 4 && !g_wgrad_v1) {  // VALU reduction (wgrad_smallco_kernel)
+  if ((cout <= 4 || (cout <= 16 && cin <= 16)) && !g_wgrad_v1) {  // VALU reduction (wgrad_smallco_kernel)
+    const int cg = cout <= 4 ? 4 : 1;  // input channels per workgroup (accumulators: cout x cg x 9)
     a.tiles_x = cdiv(W, SC_TW);
     a.tiles_y = cdiv(H, SC_TH);
     a.ntiles = (int64_t)a.tiles_x * a.tiles_y * n;
-    const int groups = cdiv(cin, SC_CG);
+    const int groups = cdiv(cin, cg);
     int64_t splits = std::max<int64_t>(1, std::min<int64_t>(a.ntiles, (2048 + groups - 1) / groups));
     a.tiles_per_block = (a.ntiles + splits - 1) / splits;
     splits = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
     const int64_t nb = splits * groups;
     if (nb >= 0x7fffffff) return AST_E_SHAPE;
+    const dim3 grid((unsigned)nb);
     if (cout <= 3) {
-      if (upsample == 2) hipLaunchKernelGGL((wgrad_smallco_kernel<3, 2>), dim3((unsigned)nb), dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((wgrad_smallco_kernel<3, 1>), dim3((unsigned)nb), dim3(256), 0, s, a);
+      if (upsample == 2) hipLaunchKernelGGL((wgrad_smallco_kernel<3, 4, 2>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((wgrad_smallco_kernel<3, 4, 1>), grid, dim3(256), 0, s, a);
+    } else if (cout == 4) {
+      if (upsample == 2) hipLaunchKernelGGL((wgrad_smallco_kernel<4, 4, 2>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((wgrad_smallco_kernel<4, 4, 1>), grid, dim3(256), 0, s, a);
     } else {
-      if (upsample == 2) hipLaunchKernelGGL((wgrad_smallco_kernel<4, 2>), dim3((unsigned)nb), dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((wgrad_smallco_kernel<4, 1>), dim3((unsigned)nb), dim3(256), 0, s, a);
+      if (upsample == 2) hipLaunchKernelGGL((wgrad_smallco_kernel<16, 1, 2>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((wgrad_smallco_kernel<16, 1, 1>), grid, dim3(256), 0, s, a);
     }
     return (int)hipGetLastError();
   }

@@ -92,6 +92,8 @@ DEC_CASES = [
     (2, 16, 9, 37, 3, 2, False),    # Cout <= 4: the VALU weight-gradient kernel, upsampled, ragged
     (1, 5, 7, 9, 4, 1, True),       # Cout = 4, Cin not a multiple of its channel group
     (2, 16, 40, 70, 3, 1, False),
+    (2, 3, 12, 20, 16, 1, False),   # Cout <= 16 with Cin <= 16: VALU kernel, one input channel per group
+    (1, 16, 9, 13, 16, 2, True),
     (1, 4, 2, 2, 64, 1, True),      # smallest reflect-padded map
     (1, 12, 1, 3, 64, 2, True),     # upsampled 1-row map
     # aligned shapes (Cin, Cout % 64 == 0, W % 32 == 0): the prefetching wgrad2 kernel
