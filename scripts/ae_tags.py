@@ -28,6 +28,10 @@ for tag, fl, ms in timer.results():
     a[2] += 1
 tot = sum(a[1] for a in agg.values()) / 5
 print(f"timed launches: {tot:.2f} ms/step")
-for tag, (fl, ms, n) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
+fam = defaultdict(float)
+for tag, (fl, ms, n) in agg.items():
+    fam[" ".join(tag.split()[:2]) if tag.startswith("mbgemm") else tag.split()[0]] += ms / 5
+print({k: round(v, 3) for k, v in sorted(fam.items(), key=lambda kv: -kv[1])})
+for tag, (fl, ms, n) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:60]:
     tf = fl / (ms * 1e-3) / 1e12 if fl > 0 else float("nan")
     print(f"{ms / 5:8.3f} ms/step {n // 5:4d}x  {tf:7.1f} TF  {tag}")
