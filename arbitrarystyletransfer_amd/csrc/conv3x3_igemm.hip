@@ -572,6 +572,115 @@ __global__ __launch_bounds__(256, 3) void conv3x3_smallc_kernel(ConvArgs a) {
   }
 }
 
+// Direct (VALU) 3x3 conv for cin <= 4 — VGG conv_1 (3->64, models.py:199-216, with the
+// Normalization of models.py:120-131 applied in the gather). As an implicit GEMM its K = 27 runs
+// in 4-channel K-chunks behind 64-channel MFMA tiles and the launch is bound by writing 21x its
+// input bytes; here a workgroup stages its 8x128-pixel source tile (+halo) once, each thread keeps
+// its 3x6 input window per channel in registers and loops over the output channels 8 at a time:
+// weights are wave-uniform (read once per wave, broadcast), every store is a 512-B row run.
+template <int CIN, bool NORM, int TH, bool NTS, int OCC>
+__global__ __launch_bounds__(TH * 32, OCC) void conv3x3_cin4_kernel(ConvArgs a, const float* __restrict__ wp) {
+  // (wp as a noalias kernel argument: the uniform weight reads become scalar loads)
+  constexpr int NT = TH * 32, TWS = 128, COG = 4;
+  constexpr int SR = TH + 2, RS = TWS + 8, C0 = 4;
+  __shared__ __attribute__((aligned(16))) float As[CIN * SR * RS];
+
+  const int tid = threadIdx.x;
+  const int tx = tid & 31, ty = tid >> 5;
+  int t = blockIdx.x;
+  const int bx = t % a.tiles_x;
+  t /= a.tiles_x;
+  const int by = t % a.tiles_y;
+  const int n = t / a.tiles_y;
+  const int x0 = bx * TWS, y0 = by * TH;
+  const int H = a.H, W = a.W;
+  const float* __restrict__ xin =
+      n < a.nsplit ? a.x + (int64_t)n * a.Cin * H * W : a.x2 + (int64_t)(n - a.nsplit) * a.Cin * H * W;
+  const int plane = H * W;
+
+  // Source tile, normalised; zero for zero padding and for channels past Cin (padding is
+  // applied to the normalised image, as the reference pads after Normalization).
+  for (int e = tid; e < CIN * SR * (TWS + 2); e += NT) {
+    const int col = e % (TWS + 2);
+    const int cr = e / (TWS + 2);
+    const int r = cr % SR, c = cr / SR;
+    const int sy = src_index<1>(y0 - 1 + r, H, a.reflect);
+    const int sx = src_index<1>(x0 - 1 + col, W, a.reflect);
+    float v = 0.f;
+    if (c < a.Cin && sy >= 0 && sx >= 0) {
+      v = xin[c * plane + sy * W + sx];
+      if (NORM) v = (v - a.in_mean[c]) / a.in_std[c];
+    }
+    As[cr * RS + C0 - 1 + col] = v;
+  }
+  __syncthreads();
+
+  float v[CIN][3][6];
+#pragma unroll
+  for (int c = 0; c < CIN; ++c)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int m = 0; m < 6; ++m) v[c][ky][m] = As[(c * SR + ty + ky) * RS + C0 - 1 + 4 * tx + m];
+
+  const int yy = y0 + ty, xx = x0 + 4 * tx;
+  const bool ok = yy < H && xx < W;
+  const bool full = ((W & 3) == 0) && xx + 3 < W;
+  const int64_t obase = (int64_t)n * a.Cout * plane + (int64_t)yy * W + xx;
+  const int cout_pad = a.cout_pad;
+  for (int co0 = 0; co0 < a.Cout; co0 += COG) {  // cout_pad is a multiple of COG: slab reads in bounds
+    float acc[COG][4];
+#pragma unroll
+    for (int k = 0; k < COG; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[k][j] = 0.f;
+#pragma unroll
+    for (int c = 0; c < CIN; ++c)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const float* wr = wp + (c * 9 + ky * 3 + kx) * cout_pad + co0;
+#pragma unroll
+          for (int k = 0; k < COG; ++k) {
+            const float w = wr[k];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[k][j] = fmaf(v[c][ky][j + kx], w, acc[k][j]);
+          }
+        }
+    if (!ok) continue;
+#pragma unroll
+    for (int k = 0; k < COG; ++k) {
+      const int co = co0 + k;
+      if (co >= a.Cout) break;
+      const float bv = a.bias ? a.bias[co] : 0.f;
+      float o[4], u[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = acc[k][j] + bv;
+        u[j] = relu_f(o[j]);
+      }
+      const int64_t off = obase + (int64_t)co * plane;
+      if (a.y_pre) {
+        if (full) {
+          if (NTS) __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4*>(a.y_pre + off));
+          else *reinterpret_cast<float4*>(a.y_pre + off) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+          for (int j = 0; j < 4; ++j) if (xx + j < W) a.y_pre[off + j] = o[j];
+        }
+      }
+      if (a.y_act) {
+        if (full) {
+          if (NTS) __builtin_nontemporal_store(f32x4{u[0], u[1], u[2], u[3]}, reinterpret_cast<f32x4*>(a.y_act + off));
+          else *reinterpret_cast<float4*>(a.y_act + off) = make_float4(u[0], u[1], u[2], u[3]);
+        } else {
+          for (int j = 0; j < 4; ++j) if (xx + j < W) a.y_act[off + j] = u[j];
+        }
+      }
+    }
+  }
+}
+
 __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ wp, int cout, int cin,
                                     int cout_pad, int cin_pad) {
   const int64_t total = (int64_t)cin_pad * 9 * cout_pad;
@@ -630,6 +739,26 @@ int launch_smallc(const ConvArgs& a0, hipStream_t s, int up) {
   return (int)hipGetLastError();
 }
 
+template <int TH, bool NTS, int OCC = 1>
+int launch_cin4(const ConvArgs& a0, hipStream_t s, int up) {
+  ConvArgs a = a0;
+  if (a.Cin > 4 || a.y_pool || up != 1) return AST_E_UNSUPPORTED;
+  a.tiles_x = cdiv(a.W, 128);
+  a.tiles_y = cdiv(a.H, TH);
+  const int64_t nblk = (int64_t)a.tiles_x * a.tiles_y * a.N;
+  if (nblk >= 0x7fffffff) return AST_E_SHAPE;
+  const dim3 g((unsigned)nblk), b(TH * 32);
+  const bool norm = a.in_mean != nullptr;
+  if (a.Cin == 3) {
+    if (norm) hipLaunchKernelGGL((conv3x3_cin4_kernel<3, true, TH, NTS, OCC>), g, b, 0, s, a, a.wp);
+    else hipLaunchKernelGGL((conv3x3_cin4_kernel<3, false, TH, NTS, OCC>), g, b, 0, s, a, a.wp);
+  } else {
+    if (norm) hipLaunchKernelGGL((conv3x3_cin4_kernel<4, true, TH, NTS, OCC>), g, b, 0, s, a, a.wp);
+    else hipLaunchKernelGGL((conv3x3_cin4_kernel<4, false, TH, NTS, OCC>), g, b, 0, s, a, a.wp);
+  }
+  return (int)hipGetLastError();
+}
+
 struct CfgEntry {
   int (*fn)(const ConvArgs&, hipStream_t, int);
   int bn;        // output channels per workgroup (weight-slab width)
@@ -659,6 +788,12 @@ const CfgEntry kConfigs[] = {
     {launch_cfg<4, 1, 2, 2, 4, true>, 64, 8, 2, 0},    // 15: as 1
     {launch_cfg<8, 2, 2, 2, 4>, 128, 16, 2, 0},        // 16: 16x32 px x 128 ch, CK 4, 16 waves (1 WG/CU)
     {launch_cfg<8, 2, 2, 2, 4, true>, 128, 16, 2, 0},  // 17: as 16, swapped
+    {launch_cin4<8, false>, 64, 8, 1, 0},               // 18: direct VALU conv, cin <= 4, no pool/upsample
+    {launch_cin4<16, false>, 64, 16, 1, 0},             // 19: as 18, 16-row tiles
+    {launch_cin4<8, true>, 64, 8, 1, 0},                // 20: as 18, nontemporal stores
+    {launch_cin4<4, false>, 64, 4, 1, 0},               // 21: as 18, 4-row tiles
+    {launch_cin4<16, true>, 64, 16, 1, 0},              // 22: 16-row tiles, nontemporal stores
+    {launch_cin4<32, true>, 64, 32, 1, 0},              // 23: 32-row tiles, nontemporal stores
 };
 constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 

@@ -95,6 +95,8 @@ def main():
         table = json.load(open(path))
     report = []
     todo = ae_shapes() if os.environ.get("TUNE_AE") else shapes(batch)
+    if os.environ.get("TUNE_SMALL"):  # only the shapes the direct VALU kernels serve (cin or cout <= 4)
+        todo = [t for t in todo if t[1] <= 4 or t[4] <= 4]
     for shp in todo:
         n, cin, h, w, cout, up, pad, pool = shp
         x = torch.from_numpy(synth.image(5, (n, cin, h, w))).to(dev)

@@ -59,6 +59,12 @@ CONV_CASES = [
     (1, 64, 32, 96, 3, 1, "reflect", False),  # final decoder conv (cout 3)
     (1, 12, 6, 10, 64, 1, "reflect", False),  # W % 4 != 0: scalar gather path
     (1, 40, 33, 64, 64, 1, "zeros", False),   # odd H, cin not a multiple of the K chunk
+    (1, 3, 9, 130, 16, 1, "reflect", False),  # cin 3, cout 16 (MobileNet block 0 class), W % 4 != 0, 2 x-tiles
+    (2, 4, 12, 64, 24, 1, "zeros", False),   # cin 4, cout 24
+    (1, 1, 5, 36, 64, 1, "reflect", False),   # cin 1 (zero channels of the 4-channel template)
+    (2, 3, 16, 256, 64, 1, "zeros", True),    # conv_1: full 128-px tiles, normalised gather
+    (1, 18, 8, 256, 3, 1, "reflect", False),  # cout 3, vector-staged tiles, partial last K chunk
+    (1, 10, 6, 128, 4, 2, "reflect", False),  # cout 4, upsampled, vector-staged tiles
 ]
 
 
