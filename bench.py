@@ -449,7 +449,7 @@ def main():
         "config": {"workload": f"config 2: VGG19-relu4_1 encoder (content+style) -> AdaIN -> mirrored decoder, "
                                f"bs={B}/GPU {S}x{S} fp32 forward",
                    "global_batch": B * world, "image_size": S, "parallelism": f"batch-sharded x{world}"},
-        "roofline": {"bound": "mfma", "kernel": "conv3x3_f32_kernel (all conv launches of a step)",
+        "roofline": {"bound": "mfma", "kernel": "conv3x3 launches of a step (16 MFMA implicit-GEMM + direct VALU conv_1 and 64->3 image conv)",
                      "achieved": achieved_tf, "peak": PEAK_FP32_MFMA_TF, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP32_MFMA_TF, "traffic": traffic,
                      "avg_launch_ms": avg_ms, "avg_launch_gflop": avg_flops / 1e9,
