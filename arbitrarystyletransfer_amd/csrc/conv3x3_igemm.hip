@@ -797,9 +797,10 @@ const CfgEntry kConfigs[] = {
 };
 constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
-int auto_config(int cout, int n, int h, int w) {
+int auto_config(int cin, int cout, int n, int h, int w, int up, bool pool) {
   if (cout <= 3) return 10;
   if (cout <= 4) return 11;
+  if (cin <= 4 && up == 1 && !pool) return 20;  // direct conv: image-input convs (conv_1)
   // 16x32 px x 64 ch, 8 waves: fastest on every VGG shape measured (profiles/, conv_tuning.json);
   // the 4-wave 8x32 tile when that leaves too few workgroups to fill 256 CUs.
   const long tiles = (long)n * cdiv(h, 16) * cdiv(w, 32) * cdiv(cout, 64);
@@ -845,7 +846,7 @@ int ast_conv3x3_fwd_f32_cfg(int cfg, const float* x, const float* x2, int n2, co
   if (pad_mode == 1 && (H < 2 || W < 2)) return AST_E_SHAPE;  // ReflectionPad2d(1) needs size >= 2
   if ((int64_t)cin * h_in * w_in >= ((int64_t)1 << 31)) return AST_E_SHAPE;         // per-image offsets are 32-bit
   if ((int64_t)round_up(cin, kCinAlign) * 9 * round_up(cout, kCoutAlign) >= ((int64_t)1 << 31)) return AST_E_SHAPE;
-  if (cfg < 0) cfg = auto_config(cout, n + n2, H, W);
+  if (cfg < 0) cfg = auto_config(cin, cout, n + n2, H, W, upsample, y_pool != nullptr);
   if (cfg >= kNumConfigs) return AST_E_UNSUPPORTED;
   const CfgEntry& e = kConfigs[cfg];
   if (y_pool && (e.rm % 2 != 0 || e.max_cout)) return AST_E_UNSUPPORTED;
