@@ -634,12 +634,13 @@ __global__ __launch_bounds__(TH * 32, OCC) void conv3x3_cin4_kernel(ConvArgs a, 
     for (int k = 0; k < COG; ++k)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[k][j] = 0.f;
+    // tap-major, channel-minor: the MFMA kernel's accumulation order (bit-identical results)
 #pragma unroll
-    for (int c = 0; c < CIN; ++c)
+    for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
+      for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
+        for (int c = 0; c < CIN; ++c) {
           const float* wr = wp + (c * 9 + ky * 3 + kx) * cout_pad + co0;
 #pragma unroll
           for (int k = 0; k < COG; ++k) {

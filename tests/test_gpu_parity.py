@@ -234,3 +234,22 @@ def test_one_style_many_contents_stats(hip_device):
     assert rel_inf(y, ref) <= OP_TOL * 10
     assert torch.equal(t, t2)
     assert rel_inf(t, R.adain_from_stats(fc.cpu(), m[0].cpu(), sd[0].cpu())) <= OP_TOL
+
+
+@pytest.mark.parametrize("cin,pad,norm", [(3, "zeros", True), (3, "reflect", False), (4, "zeros", False)])
+def test_conv3x3_direct_cin4_matches_mfma(cin, pad, norm, hip_device):
+    """The direct cin <= 4 kernel (cfg 20) accumulates in the MFMA kernel's order (tap-major,
+    channel-minor fmaf chain), so conv_1 gives the same bits either way: swapping kernels cannot
+    move a ReLU / max-pool decision downstream (the training-step gradient test depends on it)."""
+    x = torch.from_numpy(synth.image(31 + cin, (2, cin, 24, 160))).to(hip_device)
+    wt = torch.from_numpy(synth.conv_weight(32, 64, cin, 3)).to(hip_device)
+    b = torch.from_numpy(synth.conv_bias(33, 64)).to(hip_device)
+    wp = ops.pack_conv3x3(wt)
+    mean = torch.tensor(R.IMNET_MEAN, device=hip_device)[:cin] if norm else None
+    std = torch.tensor(R.IMNET_STD, device=hip_device)[:cin] if norm else None
+    kw = dict(pad_mode=pad, in_mean=mean, in_std=std, want_pre=True, want_act=True)
+    p20, a20, _ = ops.conv3x3(x, wp, b, 64, cfg=20, **kw)
+    p7, a7, _ = ops.conv3x3(x, wp, b, 64, cfg=7, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(p20, p7), float((p20 - p7).abs().max())
+    assert torch.equal(a20, a7)
