@@ -600,18 +600,36 @@ __global__ __launch_bounds__(TH * 32, OCC) void conv3x3_cin4_kernel(ConvArgs a, 
 
   // Source tile, normalised; zero for zero padding and for channels past Cin (padding is
   // applied to the normalised image, as the reference pads after Normalization).
-  for (int e = tid; e < CIN * SR * (TWS + 2); e += NT) {
+  // (all loads issued before any LDS store: one memory latency per tile, not one per element)
+  constexpr int ST = CIN * SR * (TWS + 2), ST_T = (ST + NT - 1) / NT;
+  float sv[ST_T];
+#pragma unroll
+  for (int i = 0; i < ST_T; ++i) {
+    const int e = min(tid + i * NT, ST - 1);
     const int col = e % (TWS + 2);
     const int cr = e / (TWS + 2);
     const int r = cr % SR, c = cr / SR;
     const int sy = src_index<1>(y0 - 1 + r, H, a.reflect);
     const int sx = src_index<1>(x0 - 1 + col, W, a.reflect);
-    float v = 0.f;
-    if (c < a.Cin && sy >= 0 && sx >= 0) {
-      v = xin[c * plane + sy * W + sx];
-      if (NORM) v = (v - a.in_mean[c]) / a.in_std[c];
+    const bool ok = c < a.Cin && sy >= 0 && sx >= 0;
+    sv[i] = ok ? xin[c * plane + max(sy, 0) * W + max(sx, 0)] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < ST_T; ++i) {
+    const int e = tid + i * NT;
+    if (e < ST) {
+      const int col = e % (TWS + 2);
+      const int cr = e / (TWS + 2);
+      const int c = cr / SR;
+      float v = sv[i];
+      if (NORM) {
+        const int r = cr % SR;
+        const bool ok = c < a.Cin && src_index<1>(y0 - 1 + r, H, a.reflect) >= 0 &&
+                        src_index<1>(x0 - 1 + col, W, a.reflect) >= 0;
+        v = ok ? (v - a.in_mean[c]) / a.in_std[c] : 0.f;  // padding stays 0 after normalisation
+      }
+      As[cr * RS + C0 - 1 + col] = v;
     }
-    As[cr * RS + C0 - 1 + col] = v;
   }
   __syncthreads();
 
