@@ -67,8 +67,9 @@ __global__ void norm_finish_kernel(const float* __restrict__ partial, long long 
   if (threadIdx.x == 0) {
     const float norm = sqrtf(s);
     state[0] = norm;
+    // torch: clamp(max_norm / (norm + 1e-6), max=1) -- a NaN norm gives a NaN coefficient
     const float c = max_norm / (norm + 1e-6f);
-    state[1] = max_norm > 0.f ? (c < 1.f ? c : 1.f) : 1.f;
+    state[1] = (c < 1.f || c != c) ? c : 1.f;
   }
 }
 

@@ -19,10 +19,20 @@ from . import functional
 
 
 def shard_range(global_batch: int, rank: int, world: int):
-    """[start, stop) of this rank's images; shards differ by at most one image."""
+    """[start, stop) of this rank's images; shards differ by at most one image. Every rank must
+    get at least one image (an empty shard would reach the kernels with n = 0)."""
+    if global_batch < world:
+        raise ValueError(f"global batch {global_batch} < world size {world}: some rank would get no image")
     base, extra = divmod(global_batch, world)
     start = rank * base + min(rank, extra)
     return start, start + base + (1 if rank < extra else 0)
+
+
+def shard_weight(global_batch: int, rank: int, world: int) -> float:
+    """local / global image count: the factor a rank's batch-mean loss terms carry so that the
+    SUM over ranks of the per-rank gradients is the full-batch gradient for uneven shards too."""
+    a, b = shard_range(global_batch, rank, world)
+    return (b - a) / global_batch
 
 
 def init_from_env(backend=None, device=None):
@@ -42,7 +52,7 @@ class FlatGradArena:
     """One contiguous gradient buffer for `params`; registers each parameter's slice so the
     backward kernels write into it, and averages it across ranks in one all-reduce."""
 
-    def __init__(self, params, device=None):
+    def __init__(self, params, device=None, average=True):
         self.params = list(params)
         device = device or self.params[0].device
         total = sum(p.numel() for p in self.params)
@@ -52,6 +62,11 @@ class FlatGradArena:
         for p in self.params:
             self.slices[id(p)] = (off, p.numel(), tuple(p.shape))
             off += p.numel()
+        # average=True: AVG over ranks (equal shards, per-rank batch-mean losses: DDP). False: SUM,
+        # for trainers whose per-rank losses are already weighted by shard_weight (exact for
+        # uneven shards)
+        self.average = average
+        self._taken = set()
         self.register()
 
     def register(self):
@@ -66,9 +81,23 @@ class FlatGradArena:
         off, n, shape = self.slices[id(p)]
         return self.flat[off:off + n].view(shape)
 
+    def take(self, p):
+        """The arena slice for a weight-gradient kernel to write p's gradient into, or None when
+        it must not: the slice was already handed out in this backward (p used twice in the
+        graph) or p already holds an accumulated gradient. Reset by all_reduce / reset."""
+        if id(p) in self._taken or p.grad is not None:
+            return None
+        self._taken.add(id(p))
+        return self.view_for(p)
+
+    def reset(self):
+        self._taken.clear()
+
     def all_reduce(self, group=None):
-        """Average the arena across the group (in place). Parameters whose .grad is not a view
-        of the arena (e.g. produced by a non-HIP op) are copied in first."""
+        """Reduce the arena across the group in place (AVG, or SUM when average=False).
+        Parameters whose .grad is not a view of the arena (produced by a non-HIP op, or the sum
+        of two contributions) are copied in first."""
+        self._taken.clear()
         for p in self.params:
             if p.grad is not None and p.grad.data_ptr() != self.view_for(p).data_ptr():
                 self.view_for(p).copy_(p.grad)
@@ -76,10 +105,11 @@ class FlatGradArena:
         if not dist.is_initialized() or dist.get_world_size(group) == 1:
             return
         if dist.get_backend(group) == "nccl":
-            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=group)
+            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG if self.average else dist.ReduceOp.SUM, group=group)
         else:  # gloo (CPU tests; device tensors staged through the host) has no AVG
             all_reduce_sum(self.flat, group)
-            self.flat.div_(dist.get_world_size(group))
+            if self.average:
+                self.flat.div_(dist.get_world_size(group))
 
     def __call__(self, params=None):
         self.all_reduce()

@@ -25,23 +25,24 @@ def _empty(shape, like):
 # ------------------------------------------------------------------------------------------------
 
 class TFPackCache:
-    """Transposed+flipped weight packs (input-gradient filters), refreshed on parameter change."""
+    """Transposed+flipped weight packs (input-gradient filters), refreshed on parameter change.
 
-    def __init__(self):
-        self._c = {}
+    The pack is stored on the parameter itself (`_ast_tf_pack`), so its lifetime follows the
+    tensor: a freed model's packs go with it, and a new parameter that reuses a dead one's
+    address can never hit a stale entry."""
 
     def get(self, weight: torch.Tensor, in_scale=None) -> torch.Tensor:
         w = _dev(weight.detach(), "weight")
         key = (weight.data_ptr(), weight._version, ops.WEIGHTS_EPOCH[0],
-               None if in_scale is None else in_scale.data_ptr())
-        hit = self._c.get(id(weight))
+               None if in_scale is None else (in_scale.data_ptr(), in_scale._version))
+        hit = getattr(weight, "_ast_tf_pack", None)
         if hit is not None and hit[0] == key:
             return hit[1]
         cout, cin = int(w.shape[0]), int(w.shape[1])
         out = torch.empty(int(lib().ast_conv3x3_packed_numel(cin, cout)), device=w.device, dtype=torch.float32)
         check(lib().ast_conv3x3_pack_weights_ex_f32(ptr(w), ptr(out), cout, cin, 1, ptr(in_scale), _s(w)),
               "pack_weights_ex")
-        self._c[id(weight)] = (key, out)
+        weight._ast_tf_pack = (key, out)
         return out
 
 
@@ -57,14 +58,21 @@ def conv_input_grad_same(dy, weight, in_scale=None):
 
 
 # id(parameter) -> dp.FlatGradArena: weight gradients are written straight into the arena slice
-# (a fresh view each call, which autograd adopts as .grad without copying).
+# (a view, which autograd adopts as .grad without copying).
 GRAD_ARENA = {}
 
 
 def _grad_buffer(param, shape, like):
+    """Output buffer of a weight-gradient kernel (which overwrites it). The arena slice is handed
+    out at most once per backward (dp.FlatGradArena.take): a parameter used twice in the graph
+    (the decoder under full_losses runs on t and on f_c) gets a fresh buffer for its second
+    contribution, which autograd then sums with the first, instead of both contributions being
+    written into -- and wiping -- the same storage."""
     arena = GRAD_ARENA.get(id(param)) if param is not None else None
     if arena is not None:
-        return arena.view_for(param)
+        view = arena.take(param)
+        if view is not None:
+            return view
     return _empty(shape, like)
 
 

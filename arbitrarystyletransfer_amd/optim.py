@@ -82,28 +82,48 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        groups = []
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]
-            if not params:
-                continue
-            dev = params[0].device
+            if params:
+                groups.append((gi, group, params))
+        if not groups:
+            return loss
+        dev = groups[0][2][0].device
+        for _, _, params in groups:
             for p in params:
                 st = self.state[p]
                 if len(st) == 0:
                     st["step"] = torch.tensor(0.0)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
-            grads = [ops._dev(p.grad, "grad") for p in params]
+        tables = []
+        for gi, group, params in groups:
             table = self._tables.setdefault(gi, _Table())
+            grads = [ops._dev(p.grad, "grad") for p in params]
             nchunks = table.build([p.data for p in params], grads, [self.state[p]["exp_avg"] for p in params],
                                   [self.state[p]["exp_avg_sq"] for p in params], dev)
-            state = None
-            if self.max_grad_norm is not None:
-                state = _grad_norm_state(table, len(params), nchunks, self.max_grad_norm, dev)
-                self.last_grad_norm = state[0]
-                if self.error_if_nonfinite:
-                    _check_finite(state[0])
+            tables.append((table, nchunks))
+        state = None
+        if self.max_grad_norm is not None:
+            # clip_grad_norm_(all parameters): ONE norm over every group (train.py:292 clips
+            # self.ast.parameters() as a whole)
+            if len(groups) == 1:
+                table, nchunks = tables[0]
+                n_all = len(groups[0][2])
+            else:
+                table = self._tables.setdefault("all", _Table())
+                allp = [p for _, _, ps in groups for p in ps]
+                n_all = len(allp)
+                nchunks = table.build([p.data for p in allp], [ops._dev(p.grad, "grad") for p in allp], None, None,
+                                      dev)
+            state = _grad_norm_state(table, n_all, nchunks, self.max_grad_norm, dev)
+            self.last_grad_norm = state[0]
+            if self.error_if_nonfinite:
+                _check_finite(state[0])   # raises before any state changes (as torch's clip_grad_norm_)
+        for (gi, group, params), (table, nchunks) in zip(groups, tables):
+            for p in params:
+                self.state[p]["step"] += 1
             step = int(self.state[params[0]]["step"].item())
             b1, b2 = group["betas"]
             check(lib().ast_adam_step_f32(ptr(table.dev), len(params), nchunks, ptr(state), float(group["lr"]),

@@ -20,9 +20,13 @@ train.py:248-283, as the reference adds them to the loss:
   hist         = 1e-5 * compute_hist_loss(stylised, style)                     (:261)
   loss        += hist + org_img + out_of_range                                 (:283)
 
-Data parallel (config 4): one process per GPU, each with its own batch shard; decoder gradients
-land in one flat buffer and are averaged with a single all-reduce (RCCL over xGMI) before the
-optimizer step (dp.py).
+Data parallel (config 4): one process per GPU, each with its own shard of the global batch
+(`args.batch_size` is the global batch, as the reference's --batch_size is the batch of one step;
+dp.shard_range). Decoder gradients land in one flat buffer (dp.FlatGradArena) and are SUMMED with a
+single all-reduce (RCCL over xGMI) before clip + Adam. Each rank back-propagates its batch-mean
+terms weighted by local/global images and the batch-sum term (tv, losses.py:90-103 sums over the
+batch) unweighted, so the reduced gradient is exactly the full-batch gradient of train.py's loss,
+for uneven shards too.
 """
 from __future__ import annotations
 
@@ -73,7 +77,13 @@ class AdaINTrainer:
         self.params = [p for p in self.net.decoder.parameters()]
         self.optim = FusedAdam(self.params, lr=self.args.lr, betas=(0.9, 0.999), eps=1e-5, max_grad_norm=2.0,
                                error_if_nonfinite=True)
-        self.grad_hook = grad_hook  # called between backward and the optimizer step (DP all-reduce)
+        self.grad_hook = grad_hook  # called between backward and the optimizer step
+        self.rank, self.world = 0, 1
+        self.grad_arena = None
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            self.rank, self.world = dist.get_rank(), dist.get_world_size()
+            dp.shard_range(self.args.batch_size, self.rank, self.world)   # raises on an empty shard
+            self.grad_arena = dp.FlatGradArena(self.params, average=False)
         self.train_dict = {"content_loss": [], "style_loss": [], "lf_loss": [], "tv_loss": [], "org_img_loss": []}
         self.save_file = os.path.join(self.args.save_dir, "ast.pth")
         self.train_dict_file = os.path.join(self.args.save_dir, "ast_train_dict.json")
@@ -105,7 +115,8 @@ class AdaINTrainer:
         tv = L.tv_loss(stylized)
         content_loss = torch.stack(content_terms).sum()
         style_loss = torch.stack(style_terms).sum()
-        loss = a.content_lam * content_loss + a.style_lam * style_loss + a.lf_lam * lf_loss + a.tv_lam * tv
+        mean_terms = a.content_lam * content_loss + a.style_lam * style_loss + a.lf_lam * lf_loss
+        loss = mean_terms + a.tv_lam * tv
         out = {"loss": loss, "content_loss": content_loss, "style_loss": style_loss, "lf_loss": lf_loss,
                "tv_loss": tv, "stylized": stylized, "t": t}
         if getattr(a, "full_losses", False):
@@ -116,14 +127,32 @@ class AdaINTrainer:
             org_img_loss = torch.stack(org_terms).sum() * a.org_img_lam
             range_loss = L.out_of_range_loss(stylized, 1e8)
             hist_loss = L.compute_hist_loss(stylized, style, 1e-5)
+            mean_terms = mean_terms + hist_loss + org_img_loss + range_loss
             out["loss"] = loss + hist_loss + org_img_loss + range_loss
             out.update(org_img_loss=org_img_loss, out_of_range_loss=range_loss, hist_loss=hist_loss, org_out=org_out)
+        out["_mean_terms"] = mean_terms
         return out
+
+    def shard_weight(self, local_n):
+        """local / global images of this rank's shard (1.0 in a single process)."""
+        if self.world == 1:
+            return 1.0
+        a, b = dp.shard_range(self.args.batch_size, self.rank, self.world)
+        if local_n != b - a:
+            raise ValueError(f"rank {self.rank} holds {local_n} images, its shard of the global batch "
+                             f"{self.args.batch_size} over {self.world} ranks is {b - a}")
+        return (b - a) / self.args.batch_size
 
     def train_step(self, content, style, record=False):
         out = self.compute_losses(content, style)
         self.optim.zero_grad(set_to_none=True)
-        out["loss"].backward()
+        w = self.shard_weight(content.shape[0])
+        if w == 1.0:
+            out["loss"].backward()
+        else:   # batch-mean terms carry local/global, the batch-sum tv term is already additive
+            (w * out["_mean_terms"] + self.args.tv_lam * out["tv_loss"]).backward()
+        if self.grad_arena is not None:
+            self.grad_arena.all_reduce()
         if self.grad_hook is not None:
             self.grad_hook(self.params)
         self.optim.step()
@@ -179,10 +208,16 @@ class AutoencoderTrainer:
                                   max_grad_norm=10.0)
         # data-parallel (one process per GPU, batch-sharded): SyncBatchNorm keeps the reference's
         # whole-batch statistics, one all-reduce averages the gradient arena before clip + Adam
+        # (args.batch_size = the global batch; each rank back-propagates its batch-mean losses
+        # weighted by local/global images and the arena SUMS: the full-batch gradient, uneven
+        # shards included)
         self.grad_arena = None
+        self.rank, self.world = 0, 1
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            self.rank, self.world = dist.get_rank(), dist.get_world_size()
+            dp.shard_range(self.args.batch_size, self.rank, self.world)   # raises on an empty shard
             dp.convert_sync_batchnorm(self.model)
-            self.grad_arena = dp.FlatGradArena(list(self.model.parameters()))
+            self.grad_arena = dp.FlatGradArena(list(self.model.parameters()), average=False)
         self.save_file = os.path.join(self.args.save_dir, "ae.pth")
         self.train_dict_file = os.path.join(self.args.save_dir, "train_dict.json")
         self.train_dict = {"train_loss": [], "val_loss": [], "perp_loss": []}
@@ -201,7 +236,14 @@ class AutoencoderTrainer:
     def train_step(self, content_imgs, record=True):
         out = self.compute_losses(content_imgs)
         self.ae_optim.zero_grad(set_to_none=True)
-        out["loss"].backward()
+        if self.world == 1:
+            out["loss"].backward()
+        else:
+            a, b = dp.shard_range(self.args.batch_size, self.rank, self.world)
+            if content_imgs.shape[0] != b - a:
+                raise ValueError(f"rank {self.rank} holds {content_imgs.shape[0]} images, its shard of the global "
+                                 f"batch {self.args.batch_size} is {b - a}")
+            ((b - a) / self.args.batch_size * out["loss"]).backward()
         if self.grad_arena is not None:
             self.grad_arena.all_reduce()
         self.ae_optim.step()                                                           # clip 10 + Adam, :159-165

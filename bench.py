@@ -44,8 +44,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=None, help="images per GPU (config 2: 8, config 5: 32)")
     p.add_argument("--size", type=int, default=None, help="image side (config 2: 512, config 5: 1024)")
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(os.cpu_count(), OMP_NUM_THREADS or 16)")
+    p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline time budget (0 = skip)")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="0 = best of os.cpu_count(), the affinity/cgroup CPU share and OMP_NUM_THREADS")
     p.add_argument("--mode", choices=["fwd", "train", "mobilenet", "ae-train"], default="fwd",
                    help="fwd: config 2 (the headline metric); train: config 3/4 AdaIN training step; "
                         "mobilenet: config 5; ae-train: train_autoencoder.py step (SURVEY §8f next #4)")
@@ -60,14 +61,13 @@ def parse():
 def train_bench(args, dev, rank, world):
     """Config 3 (bs=16, 1 GPU) / config 4 (bs=8 per GPU, RCCL gradient all-reduce): one step =
     forward, loss network x3, losses, backward, all-reduce (N>1), clip + Adam."""
-    from arbitrarystyletransfer_amd import dp
     from arbitrarystyletransfer_amd.train import AdaINTrainer, default_args
     B, S = args.batch or 16, args.size or 512
-    arena = None
-    trainer = AdaINTrainer(default_args(batch_size=B, image_size=S, full_losses=args.full_losses), device=dev)
-    if world > 1:
-        arena = dp.FlatGradArena(trainer.params)
-        trainer.grad_hook = arena
+    # args.batch_size = the global batch; the trainer shards it (dp.shard_range), keeps the decoder
+    # gradient in one flat arena and sums it across ranks in one all-reduce before clip + Adam
+    trainer = AdaINTrainer(default_args(batch_size=B * world, image_size=S, full_losses=args.full_losses),
+                           device=dev)
+    assert (trainer.grad_arena is not None) == (world > 1)
     content = torch.from_numpy(synth.image(777 + 2 * rank, (B, 3, S, S))).to(dev)
     style = torch.from_numpy(synth.image(778 + 2 * rank, (B, 3, S, S))).to(dev)
     for _ in range(args.warmup):
@@ -125,7 +125,7 @@ def ae_train_bench(args, dev, rank, world):
     of the backward sums) and one gradient all-reduce over RCCL before clip + Adam."""
     from arbitrarystyletransfer_amd.train import AutoencoderTrainer, default_ae_args
     B, S = args.batch or 16, args.size or 160
-    trainer = AutoencoderTrainer(default_ae_args(batch_size=B), device=dev,
+    trainer = AutoencoderTrainer(default_ae_args(batch_size=B * world), device=dev,
                                  model=models.AutoEncoder().load_live_init())
     content = torch.from_numpy(synth.image(901 + rank, (B, 3, S, S))).to(dev)
     for _ in range(args.warmup):
@@ -176,13 +176,16 @@ def ae_train_bench(args, dev, rank, world):
 
 
 def _pmc_traffic(name):
-    """HBM bytes per launch of the dominant kernel, from the committed rocprofv3 FETCH_SIZE /
-    WRITE_SIZE passes (profiles/<name>, scripts/pmc_traffic.py); None when absent."""
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes (profiles/<name>, scripts/pmc_traffic.py), and where that number comes from.
+    PMC counters cannot be collected inside this timed run; the value is replayed from the named
+    profile, taken on the commit it records: (None, None) when absent."""
     try:
         with open(os.path.join(ROOT, "profiles", name)) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, None
+    return d.get("hbm_bytes_per_launch"), f"profiles/{name}@{d.get('commit', 'unknown')} ({d.get('source', '')})"
 
 
 def mobilenet_bench(args, dev, rank, world):
@@ -247,6 +250,8 @@ def mobilenet_bench(args, dev, rank, world):
                                    "tflops": tf, "frac_of_bf16_mfma_peak": tf / PEAK_BF16_MFMA_TF}
     step_s = elapsed / args.steps
     achieved = fused_min_bytes / step_s / 1e9
+    # PMC bytes per expand_dw launch, measured at the default B=32, 1024^2
+    mb_traffic = _pmc_traffic("mb_traffic.json") if (B, S) == (32, 1024) and not args.attention else (None, None)
     ed = fam.get("mb expand_dw")
     ed_gbs = (ed[0] / (ed[1] * 1e-3) / 1e9) if ed else None
     dw_tf = (2 * dw_fma_per_step * args.steps / (ed[1] * 1e-3) / 1e12) if ed else None
@@ -268,8 +273,7 @@ def mobilenet_bench(args, dev, rank, world):
                      "achieved": ed_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": (ed_gbs / PEAK_HBM_GBS) if ed_gbs else None,
                      # PMC bytes per expand_dw launch, measured at the default B=32, 1024^2
-                     "traffic": _pmc_traffic("mb_traffic.json") if (B, S) == (32, 1024) and not args.attention
-                     else None,
+                     "traffic": mb_traffic[0], "traffic_source": mb_traffic[1],
                      "avg_launch_ms": (ed[1] / ed[2]) if ed else None,
                      "avg_launch_gb": (ed[0] / ed[2] / 1e9) if ed else None,
                      "valu": {"dw_tflops": dw_tf, "peak": PEAK_FP32_MFMA_TF,
@@ -280,8 +284,8 @@ def mobilenet_bench(args, dev, rank, world):
         "kernels": kernels,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        threads = args.cpu_threads or min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-        result["cpu_baseline"] = cpu_baseline_mobilenet(S, args.cpu_seconds, threads, args.attention)
+        result["cpu_baseline"] = cpu_baseline_mobilenet(S, args.cpu_seconds, cpu_thread_options(args.cpu_threads),
+                                                        args.attention)
     if rank == 0:
         print(json.dumps(result), flush=True)
 
@@ -300,10 +304,56 @@ def _cpu_model():
     return f"{cpu_model}, {platform.machine()}"
 
 
-def cpu_baseline_mobilenet(size, seconds, threads, attention=False):
+def cpu_thread_options(requested: int = 0):
+    """Thread counts the CPU baseline is timed at: the host's cores (os.cpu_count()),
+    the CPUs this process may run on (affinity mask, cgroup quota) and the OMP_NUM_THREADS the box
+    sets. The best of them is reported, so a quota smaller than the core count cannot understate
+    the baseline by oversubscription, nor a thread cap by under-use."""
+    if requested:
+        return [requested]
+    n = os.cpu_count() or 1
+    opts = {n}
+    try:
+        opts.add(len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            opts.add(max(1, int(-(-int(q) // int(per)))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        opts.add(min(int(omp), n))
+    return sorted(opts, reverse=True)
+
+
+def time_cpu(run_one, seconds, thread_opts, max_items=64):
+    """Time `run_one()` (one unit of CPU work) at each thread count for seconds/len(opts) each
+    (at least one unit); returns (best rate, its threads, {threads: rate}, units, elapsed)."""
+    rates, best = {}, None
+    budget = seconds / len(thread_opts)
+    for th in thread_opts:
+        torch.set_num_threads(th)
+        run_one(warmup=True)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            run_one(warmup=False)
+            n += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget or n >= max_items:
+                break
+        rates[th] = n / dt
+        if best is None or rates[th] > best[0]:
+            best = (rates[th], th, n, dt)
+    return best[0], best[1], rates, best[2], best[3]
+
+
+def cpu_baseline_mobilenet(size, seconds, thread_opts, attention=False):
     """The CPU oracle of the MobileNet variant (fp32: the reference has no bf16 CPU path)."""
     from oracle import ref_cpu as R
-    torch.set_num_threads(threads)
     sds = []
     for m, seed in ((models.Encoder(), 5), (models.Decoder(), 6), (models.AutoEncoder().ada_out, 7)):
         sds.append(synth.live_init_(m, seed).eval().state_dict())
@@ -312,54 +362,84 @@ def cpu_baseline_mobilenet(size, seconds, threads, attention=False):
         kw["att_sds"] = [synth.live_init_(models.AdaAttN(128), seed).state_dict() for seed in (8, 9)]
     c = torch.from_numpy(synth.image(821, (1, 3, size, size)))
     s = torch.from_numpy(synth.image(822, (1, 3, size, size)))
-    with torch.no_grad():
-        R.mb_style_transfer(c[:, :, :64, :64], s[:, :, :64, :64], *sds, **kw)
-        n, t0 = 0, time.perf_counter()
-        while True:
-            R.mb_style_transfer(c, s, *sds, **kw)
-            n += 1
-            dt = time.perf_counter() - t0
-            if dt >= seconds or n >= 64:
-                break
-    return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
+
+    def one(warmup):
+        with torch.no_grad():
+            if warmup:
+                R.mb_style_transfer(c[:, :, :64, :64], s[:, :, :64, :64], *sds, **kw)
+            else:
+                R.mb_style_transfer(c, s, *sds, **kw)
+
+    rate, th, rates, n, dt = time_cpu(one, seconds, thread_opts)
+    return {"value": rate, "unit": "images/s", "cores": th, "kind": "port",
             "sample": f"{n} content+style pair(s) of 1x3x{size}x{size}, MobileNet variant, fp32 torch CPU "
-                      f"({_cpu_model()}), {dt:.1f} s"}
+                      f"({_cpu_model()}, os.cpu_count()={os.cpu_count()}), {dt:.1f} s; images/s by threads: "
+                      + ", ".join(f"{k}: {v:.3f}" for k, v in rates.items())}
 
 
-def cpu_baseline(size, seconds, threads):
-    """Time the CPU oracle on single 512^2 pairs until `seconds` of work (at least one pair)."""
+def cpu_baseline(size, seconds, thread_opts):
+    """Time the CPU oracle on single 512^2 pairs (the reference's CPU path: stock torch CPU ops)."""
     from oracle import ref_cpu as R
-    torch.set_num_threads(threads)
     enc = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_encoder_weights(1)[:9]]
     dec = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_decoder_weights(2)]
     c = torch.from_numpy(synth.image(777, (1, 3, size, size)))
     s = torch.from_numpy(synth.image(778, (1, 3, size, size)))
-    with torch.no_grad():
-        R.style_transfer(c[:, :, :64, :64], s[:, :, :64, :64], enc, dec)  # warm-up (small)
-        n, t0 = 0, time.perf_counter()
-        while True:
-            R.style_transfer(c, s, enc, dec)
-            n += 1
-            dt = time.perf_counter() - t0
-            if dt >= seconds or n >= 64:
-                break
-    import platform
-    cpu_model = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
+
+    def one(warmup):
+        with torch.no_grad():
+            if warmup:
+                R.style_transfer(c[:, :, :64, :64], s[:, :, :64, :64], enc, dec)
+            else:
+                R.style_transfer(c, s, enc, dec)
+
+    rate, th, rates, n, dt = time_cpu(one, seconds, thread_opts)
+    return {"value": rate, "unit": "images/s", "cores": th, "kind": "port",
             "sample": f"{n} content+style pair(s) of 1x3x{size}x{size}, VGG relu4_1 -> AdaIN -> decoder, "
-                      f"fp32 torch CPU ({cpu_model}, {platform.machine()}), {dt:.1f} s"}
+                      f"fp32 torch CPU ({_cpu_model()}, os.cpu_count()={os.cpu_count()}), {dt:.1f} s; "
+                      "images/s by threads: " + ", ".join(f"{k}: {v:.3f}" for k, v in rates.items())}
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` without a launcher: start N rank processes of this script (one per GPU, RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run sets them) as children, wait
+    for all, return the first non-zero exit code. This process never touches the GPU."""
+    import signal
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    code = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                pending.remove(p)
+                if rc != 0 and code == 0:
+                    code = rc
+                    for q in pending:     # one rank failed: the others would wait forever in a collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return code if code >= 0 else 128 - code
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -430,7 +510,7 @@ def main():
     adain = [(tag, -fl, ms) for tag, fl, ms in recs if tag.startswith("adain")]
     adain_gbs = (sum(b for _, b, _ in adain) / (sum(m for _, _, m in adain) * 1e-3) / 1e9) if adain else None
 
-    traffic = _pmc_traffic("conv_traffic.json")
+    traffic, traffic_src = _pmc_traffic("conv_traffic.json") if (B, S) == (8, 512) else (None, None)
 
     images = B * world * args.steps
     result = {
@@ -451,7 +531,7 @@ def main():
                    "global_batch": B * world, "image_size": S, "parallelism": f"batch-sharded x{world}"},
         "roofline": {"bound": "mfma", "kernel": "conv3x3 launches of a step (16 MFMA implicit-GEMM + direct VALU conv_1 and 64->3 image conv)",
                      "achieved": achieved_tf, "peak": PEAK_FP32_MFMA_TF, "unit": "TFLOP/s",
-                     "frac": achieved_tf / PEAK_FP32_MFMA_TF, "traffic": traffic,
+                     "frac": achieved_tf / PEAK_FP32_MFMA_TF, "traffic": traffic, "traffic_source": traffic_src,
                      "avg_launch_ms": avg_ms, "avg_launch_gflop": avg_flops / 1e9,
                      "encoder_frac": enc_tf / PEAK_FP32_MFMA_TF,
                      "encoder_conv2_9_frac": enc_main_tf / PEAK_FP32_MFMA_TF,
@@ -468,8 +548,7 @@ def main():
         result["per_layer"] = {k: {"ms": v[1] / args.steps, "tflops": v[0] / (v[1] * 1e-3) / 1e12}
                                for k, v in sorted(layers.items())}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        threads = args.cpu_threads or min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-        result["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, threads)
+        result["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, cpu_thread_options(args.cpu_threads))
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -19,7 +19,16 @@ for f in sorted(glob.glob(os.path.join(root, f"{tag}_pmc_*", "**", "*counter_col
             n[r["Counter_Name"]] += 1
 fetch = tot["FETCH_SIZE"] / max(n["FETCH_SIZE"], 1)
 write = tot["WRITE_SIZE"] / max(n["WRITE_SIZE"], 1)
-res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({tag}); mean per '{filt}' dispatch over "
+import subprocess
+try:
+    sha = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+                         cwd=os.path.dirname(root)).stdout.strip()
+    dirty = subprocess.run(["git", "status", "--porcelain", "--untracked-files=no"], capture_output=True,
+                           text=True, cwd=os.path.dirname(root)).stdout.strip()
+    commit = sha + ("+uncommitted" if dirty else "")
+except OSError:
+    commit = "unknown"
+res = {"commit": commit, "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({tag}); mean per '{filt}' dispatch over "
                  f"{n['FETCH_SIZE']} dispatches; FETCH_SIZE x2 per MI355X_MICROARCH.md gfx950 correction",
        "fetch_bytes_raw": fetch, "fetch_bytes_x2": 2 * fetch, "write_bytes": write,
        "hbm_bytes_per_launch": 2 * fetch + write}

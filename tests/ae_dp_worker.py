@@ -20,7 +20,7 @@ def main(out_path):
     g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ae_train_step_64.npz"))
     content = torch.from_numpy(g["content"])
     a, b = dp.shard_range(content.shape[0], rank, world)
-    tr = AutoencoderTrainer(default_ae_args(batch_size=b - a), device="cuda:0", model=models.AutoEncoder().load_live_init())
+    tr = AutoencoderTrainer(default_ae_args(batch_size=content.shape[0]), device="cuda:0", model=models.AutoEncoder().load_live_init())
     assert tr.grad_arena is not None
     snap = {}
     orig = tr.ae_optim.step

@@ -195,6 +195,7 @@ def main():
     ae_train_golden(R)
     mobilenet_golden(R)
     adaattn_golden(R)
+    init_golden(R)
     print("golden vectors written to", HERE)
 
 
@@ -440,8 +441,40 @@ def train_step_golden(R, enc_wb, dec_wb, full=False):
     np.savez_compressed(os.path.join(HERE, "train_step_full_64.npz" if full else "train_step_64.npz"), **out)
 
 
+INIT_BLOCKS = (   # (inp, oup, stride, expand_ratio, kernel_size, use_norm, use_identity)
+    (16, 24, 2, 6, 3, True, True),
+    (40, 40, 1, 6, 5, True, True),
+    (24, 24, 1, 1, 3, False, True),
+    (256, 128, 1, 6, 3, False, False),
+)
+
+
+def init_golden(R):
+    """A14: DepthWiseConv._initialize_weights (mobilenetv2.py:168-181) and the constructor-order RNG
+    draws of the reference's own modules, under fixed torch.manual_seed: per state-dict entry the
+    first 64 values and a checksum, for single blocks and for the whole AutoEncoder
+    (models.py:322-338: Encoder + ada_out + Decoder, 434 keys)."""
+    out = {}
+    for i, (inp, oup, stride, ratio, k, norm, ident) in enumerate(INIT_BLOCKS):
+        torch.manual_seed(100 + i)
+        m = R["DepthWiseConv"](inp, oup, stride, ratio, kernel_size=k, use_norm=norm, use_identity=ident)
+        for key, v in m.state_dict().items():
+            if v.dtype.is_floating_point:
+                out[f"block{i}:{key}:head"] = v.flatten()[:64].numpy()
+                out[f"block{i}:{key}:sum"] = synth.checksum(v.numpy())
+    torch.manual_seed(7)
+    ae = R["AutoEncoder"]()
+    for key, v in ae.state_dict().items():
+        if v.dtype.is_floating_point:
+            out[f"ae:{key}:head"] = v.flatten()[:16].numpy()
+            out[f"ae:{key}:sum"] = synth.checksum(v.numpy())
+    np.savez_compressed(os.path.join(HERE, "mb_init.npz"), **out)
+
+
 if __name__ == "__main__":
-    if "--mobilenet" in sys.argv:
+    if "--init" in sys.argv:
+        init_golden(load_reference())
+    elif "--mobilenet" in sys.argv:
         torch.manual_seed(0)
         mobilenet_golden(load_reference())
     elif "--adaattn" in sys.argv:

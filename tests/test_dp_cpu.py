@@ -18,7 +18,9 @@ def test_shard_range():
     assert [dp.shard_range(64, r, 8) for r in range(8)] == [(8 * r, 8 * r + 8) for r in range(8)]
     spans = [dp.shard_range(10, r, 4) for r in range(4)]
     assert spans == [(0, 3), (3, 6), (6, 8), (8, 10)]
-    assert [dp.shard_range(3, r, 4) for r in range(4)] == [(0, 1), (1, 2), (2, 3), (3, 3)]
+    with pytest.raises(ValueError):   # an empty shard is refused (advisor r1)
+        dp.shard_range(3, 3, 4)
+    assert [dp.shard_weight(10, r, 4) for r in range(4)] == [0.3, 0.3, 0.2, 0.2]
 
 
 def _free_port():

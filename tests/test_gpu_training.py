@@ -348,3 +348,76 @@ def test_train_step_full_losses_golden(golden, hip_device):
     torch.autograd.backward([R.vgg_decoder(t, dec), R.vgg_decoder(f_c, dec)], grad_tensors=[xs.grad, xo.grad])
     for i, (gr, p) in enumerate(zip(snap["grads"], params)):
         assert rel_inf(gr, p.grad) <= 2e-4, (i, rel_inf(gr, p.grad))
+
+
+def _single_process_step(d, global_batch, size, full, arena=False):
+    """One AdaINTrainer step over the whole batch in this process: (grads, params, grad_norm)."""
+    from arbitrarystyletransfer_amd.dp import FlatGradArena
+    from arbitrarystyletransfer_amd.train import AdaINTrainer, default_args
+    content = torch.from_numpy(synth.image(941, (global_batch, 3, size, size))).to(d)
+    style = torch.from_numpy(synth.image(942, (global_batch, 3, size, size))).to(d)
+    snap = {}
+
+    def hook(params):
+        snap["grads"] = [p.grad.detach().clone() for p in params]
+
+    tr = AdaINTrainer(default_args(batch_size=global_batch, full_losses=full), device=d, grad_hook=hook)
+    if arena:   # the arena a data-parallel run uses, here in one process (world size 1)
+        tr.grad_arena = FlatGradArena(tr.params, average=False)
+    try:
+        out = tr.train_step(content, style)
+    finally:
+        if arena:
+            tr.grad_arena.unregister()
+    return snap["grads"], [p.detach().clone() for p in tr.params], float(out["grad_norm"])
+
+
+def test_full_losses_step_with_grad_arena(hip_device):
+    """advisor r1 (high): with full_losses the decoder runs twice (t and f_c), so each decoder
+    weight gets two gradient contributions. With the DP gradient arena registered, both must still
+    be summed (the arena slice is handed out once per backward), i.e. the same gradient as without
+    the arena (up to the run-to-run order of the weight-gradient kernel's atomics; the bug gave
+    2*dW2 in place of dW1 + dW2)."""
+    g0, p0, n0 = _single_process_step(hip_device, 2, 32, True, arena=False)
+    g1, p1, n1 = _single_process_step(hip_device, 2, 32, True, arena=True)
+    for i, (a, b) in enumerate(zip(g0, g1)):
+        assert rel_inf(b, a) <= 1e-5, (i, rel_inf(b, a))
+    np.testing.assert_allclose(n1, n0, rtol=1e-6)
+    for a, b in zip(p0, p1):
+        diff = np.abs((a - b).cpu().numpy())
+        assert np.mean(diff > 1e-6) <= 1e-3 and diff.max() <= 4e-4
+
+
+@pytest.mark.parametrize("global_batch,full", [(3, False), (2, True)])
+def test_adain_dp_two_ranks_match_single_process(global_batch, full, tmp_path, hip_device):
+    """BASELINE.json config 4 on the HIP path: two ranks
+    (torch.distributed.run, gloo on the one GPU) each run AdaINTrainer on their shard of the global
+    batch (3 images: uneven 2 + 1 shards; 2 images with the full train.py loss), the decoder
+    gradients meet in dp.FlatGradArena's one all-reduce, then clip + Adam. The reduced gradient and
+    the updated weights must equal one process stepping the whole batch (train.py:287-300)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    size = 64
+    out = str(tmp_path / "dp.npz")
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "adain_dp_worker.py")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", worker, out, str(global_batch), str(size)]
+                       + (["full"] if full else []), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    got = np.load(out)
+    grads, params, norm = _single_process_step(hip_device, global_batch, size, full)
+    # the per-image forward is identical on both sides; only the batch split of the gradient sums
+    # differs (fp32 reassociation)
+    for i, g in enumerate(grads):
+        assert rel_inf(got[f"grad{i}"], g) <= 1e-4, (i, rel_inf(got[f"grad{i}"], g))
+    np.testing.assert_allclose(float(got["grad_norm"]), norm, rtol=1e-5)
+    for i, p in enumerate(params):
+        diff = np.abs(got[f"param{i}"] - p.cpu().numpy())
+        # Adam's first step is ~lr*sign(g): elements whose gradient is within rounding of 0 may differ
+        assert np.mean(diff > 1e-6) <= 1e-3 and diff.max() <= 4e-4, (i, np.mean(diff > 1e-6), diff.max())

@@ -253,3 +253,36 @@ def test_hist_oracle_matches_reference(golden):
     r.backward()
     assert abs(float(r) - float(g["range_loss"])) <= 1e-6 * abs(float(g["range_loss"]))
     assert rel_inf(x.grad, g["range_grad"]) < 1e-6
+
+
+def test_mobilenet_init_matches_reference():
+    """A14: DepthWiseConv._initialize_weights (mobilenetv2.py:168-181) and the
+    module construction order (which fixes the RNG draw order) reproduce the reference's own
+    modules under the same torch.manual_seed, bit for bit (tests/golden/mb_init.npz, made by
+    make_golden.py --init from the reference's classes): single blocks of every kind and the whole
+    AutoEncoder (models.py:322-338)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_golden import INIT_BLOCKS
+    from arbitrarystyletransfer_amd import mobilenetv2, models, synth
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mb_init.npz"))
+    checked = 0
+    for i, (inp, oup, stride, ratio, k, norm, ident) in enumerate(INIT_BLOCKS):
+        torch.manual_seed(100 + i)
+        m = mobilenetv2.DepthWiseConv(inp, oup, stride, ratio, kernel_size=k, use_norm=norm, use_identity=ident)
+        for key, v in m.state_dict().items():
+            if v.dtype.is_floating_point:
+                np.testing.assert_array_equal(v.flatten()[:64].numpy(), g[f"block{i}:{key}:head"], err_msg=key)
+                np.testing.assert_array_equal(synth.checksum(v.numpy()), g[f"block{i}:{key}:sum"], err_msg=key)
+                checked += 1
+    torch.manual_seed(7)
+    ae = models.AutoEncoder()
+    keys = [k for k, v in ae.state_dict().items() if v.dtype.is_floating_point]
+    assert sorted(f"ae:{k}:sum" for k in keys) == sorted(k for k in g.files if k.startswith("ae:") and k.endswith(":sum"))
+    for key in keys:
+        v = ae.state_dict()[key]
+        np.testing.assert_array_equal(v.flatten()[:16].numpy(), g[f"ae:{key}:head"], err_msg=key)
+        np.testing.assert_array_equal(synth.checksum(v.numpy()), g[f"ae:{key}:sum"], err_msg=key)
+        checked += 1
+    assert checked > 300
