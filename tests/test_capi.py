@@ -94,3 +94,27 @@ def test_data_loader_module_mirrors_reference_names():
                  "get_transform", "image_loader", "infinite_sampler", "InfiniteSamplerWrapper",
                  "FlatFolderDataset", "FlatFolderDatasetAE"):
         assert hasattr(DL, name), name
+
+
+def test_torch_ops_registered_with_meta_kernels():
+    """torch.ops.ast_hip.* (csrc/torch_ops.cpp over the same C ABI) loads without a
+    GPU, every op has a schema, and the Meta kernels give the HIP kernels' output shapes."""
+    import torch
+    from arbitrarystyletransfer_amd import torch_ops
+    o = torch_ops.load()
+    for name in torch_ops.OPS:
+        assert hasattr(o, name), name
+    m = torch.device("meta")
+    x = torch.empty(2, 16, 8, 12, device=m)
+    assert o.adain(x, torch.empty(2, 16, 5, 7, device=m), 0.5, True).shape == x.shape
+    mean, std = o.channel_stats(x, True, 0.0)
+    assert mean.shape == std.shape == (2, 16, 1, 1)
+    pk = o.conv3x3_pack(torch.empty(64, 16, 3, 3, device=m))
+    assert pk.numel() == _lib.lib().ast_conv3x3_packed_numel(64, 16)
+    pre, act, pool = o.conv3x3_fwd(x, pk, None, 64, 2, 1, None, None, True, False, True, -1)
+    assert pre.shape == (2, 64, 16, 24) and act.numel() == 0 and pool.shape == (2, 64, 8, 12)
+    assert o.gram(x).shape == (2, 16, 16)
+    with pytest.raises(RuntimeError):   # schema/shape errors raise, as the reference's torch ops
+        o.conv3x3_fwd(x, pk, None, 128, 1, 0, None, None, True, False, False, -1)
+    with pytest.raises(NotImplementedError):   # no CPU kernel: there is no CPU fallback
+        o.adain(torch.zeros(1, 2, 3, 3), torch.zeros(1, 2, 3, 3), 1.0, True)

@@ -253,3 +253,40 @@ def test_conv3x3_direct_cin4_matches_mfma(cin, pad, norm, hip_device):
     torch.cuda.synchronize()
     assert torch.equal(p20, p7), float((p20 - p7).abs().max())
     assert torch.equal(a20, a7)
+
+
+def test_torch_ops_equal_ctypes_path(hip_device):
+    """torch.ops.ast_hip.* (the dispatcher registration, csrc/torch_ops.cpp) launches the same
+    kernels as the ctypes binding: outputs are bit-identical (VERDICT r1 next #6)."""
+    from arbitrarystyletransfer_amd import ops, torch_ops
+    o = torch_ops.load()
+    d = hip_device
+    c = torch.from_numpy(synth.image(3, (2, 64, 24, 40))).to(d) * 3 + 1
+    s = torch.from_numpy(synth.image(4, (2, 64, 17, 9))).to(d) * 2
+    for alpha, swap in ((1.0, True), (0.4, False)):
+        assert torch.equal(o.adain(c, s, alpha, swap), ops.adain(c, s, alpha=alpha, swap_style_stats=swap))
+    for unb, eps in ((True, 0.0), (True, 1e-5), (False, 0.0)):
+        a, b = o.channel_stats(c, unb, eps), ops.channel_stats(c, unb, eps)
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    w = torch.from_numpy(synth.conv_weight(5, 128, 64, 3)).to(d)
+    bias = torch.from_numpy(synth.conv_bias(6, 128)).to(d)
+    pk = o.conv3x3_pack(w)
+    assert torch.equal(pk, ops.pack_conv3x3(w))
+    for up, pad, pool in ((1, 0, True), (2, 1, False)):
+        got = o.conv3x3_fwd(c, pk, bias, 128, up, pad, None, None, True, True, pool, -1)
+        ref = ops.conv3x3(c, pk, bias, 128, upsample=up, pad_mode=("zeros", "reflect")[pad], want_pre=True,
+                          want_act=True, want_pool=pool, cfg=-1, _pack=False)
+        for g, r in zip(got, ref):
+            assert (r is None and g.numel() == 0) or torch.equal(g, r)
+    img = torch.from_numpy(synth.image(7, (2, 3, 40, 36))).to(d)
+    w1 = torch.from_numpy(synth.conv_weight(8, 64, 3, 3)).to(d)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=d)
+    std = torch.tensor([0.229, 0.224, 0.225], device=d)
+    got = o.conv3x3_fwd(img, o.conv3x3_pack(w1), None, 64, 1, 0, mean, std, True, True, False, -1)
+    ref = ops.conv3x3(img, ops.pack_conv3x3(w1), None, 64, in_mean=mean, in_std=std, want_pre=True, want_act=True,
+                      cfg=-1, _pack=False)
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+    f = torch.from_numpy(synth.image(9, (2, 64, 32, 32))).to(d)
+    from arbitrarystyletransfer_amd import losses as L
+    g1 = o.gram(f)
+    assert rel_inf(g1, L.gram_matrix(f)) <= 1e-6   # split-K atomics: order may differ run to run
