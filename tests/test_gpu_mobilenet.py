@@ -225,6 +225,50 @@ def check_bf16_segments(ast, c, s, enc_sd, dec_sd, ada_sd, dev):
         assert rel_inf(ast.encode(d(c), d(s)), tr) <= BF16_E2E_T_TOL
 
 
+BF16_E2E_TOL = 2e-2   # bf16 HIP path end to end vs the bf16-storage oracle
+
+
+def check_bf16_end_to_end(ast, c, s, enc_sd, dec_sd, ada_sd, dev):
+    """What the bf16 HIP path actually produces (bench --mode mobilenet) against the oracle that
+    rounds to bf16 where the HIP path stores bf16 (R.mb_style_transfer_bf16):
+      * the image, end to end: BF16_E2E_TOL;
+      * the encoder maps (layers 12, 14 of content and style), end to end: BF16_E2E_TOL;
+      * t (the decoder input) from the HIP path's own encoder maps: BF16_E2E_TOL.
+    t end to end is ill-conditioned, not inaccurate: AdaIN divides by content stds down to ~4e-3,
+    so a one-ulp bf16 flip of an encoder output moves t by several percent. Its bound is stated
+    against the same spread between two oracles that differ only in rounding order (the fp32
+    oracle rounded to bf16 at the encoder outputs vs the bf16-storage oracle): <= 3x that spread."""
+    bf = torch.bfloat16
+    with torch.no_grad():
+        yr, tr = R.mb_style_transfer_bf16(c, s, enc_sd, dec_sd, ada_sd, exporting=True, return_t=True)
+        # AST.forward(exporting) step by step (models.py AST.encode: encoder x2 -> per-layer AdaIN ->
+        # ada_out; then the decoder), keeping the encoder maps of this very run: the SE pool sums
+        # are float atomics, so a second run may differ in the last bits, which AdaIN amplifies
+        ce, se = ast._enc(c.to(dev).to(bf), out_layers=[12, 14]), ast._enc(s.to(dev).to(bf), out_layers=[12, 14])
+        t = ast.ada_out(*ast.stylize_maps(ce, se))
+        y = ast._dec(t)
+        cr, sr = R.mb_encoder_bf16(c, enc_sd), R.mb_encoder_bf16(s, enc_sd)
+        e_enc = max(rel_inf(a, b) for a, b in zip(ce + se, cr + sr))
+        t_own = R.mb_block_bf16(torch.cat([R.bf16(R.adain(ce[i].float().cpu(), se[i].float().cpu())) for i in range(2)], 1),
+                                ada_sd, "", 256, 128, 1, 3, 3, use_norm=False, use_identity=False)
+        c32, s32 = R.mb_encoder(c, enc_sd), R.mb_encoder(s, enc_sd)
+        t_alt = R.mb_block_bf16(torch.cat([R.bf16(R.adain(R.bf16(c32[i]), R.bf16(s32[i]))) for i in range(2)], 1),
+                                ada_sd, "", 256, 128, 1, 3, 3, use_norm=False, use_identity=False)
+    ey, et_own, et, spread = rel_inf(y, yr), rel_inf(t, t_own), rel_inf(t, tr), rel_inf(t_alt, tr)
+    print(f"bf16 vs bf16-storage oracle: image {ey:.2e}, encoder maps {e_enc:.2e}, t from own maps {et_own:.2e}, "
+          f"t end to end {et:.2e} (oracle-vs-oracle spread {spread:.2e})")
+    assert ey <= BF16_E2E_TOL and e_enc <= BF16_E2E_TOL and et_own <= BF16_E2E_TOL, (ey, e_enc, et_own)
+    assert et <= max(BF16_E2E_TOL, 3 * spread), (et, spread)
+
+
+@pytest.mark.parametrize("name", ["mb_path_64", "mb_path_128x96"])
+def test_bf16_end_to_end(name, golden, hip_device):
+    g = golden(name)
+    c, s = _inputs(g)
+    ast, enc_sd, dec_sd, ada_sd = _nets(hip_device, torch.bfloat16)
+    check_bf16_end_to_end(ast, c, s, enc_sd, dec_sd, ada_sd, hip_device)
+
+
 def test_bf16_path_64(golden, hip_device):
     g = golden("mb_path_64")
     c, s = _inputs(g)
@@ -240,6 +284,7 @@ def test_config5_shape_bf16_1024(hip_device):
     ast, enc_sd, dec_sd, ada_sd = _nets(hip_device, torch.bfloat16)
     torch.set_num_threads(16)
     check_bf16_segments(ast, c[1:].float(), s[1:].float(), enc_sd, dec_sd, ada_sd, hip_device)
+    check_bf16_end_to_end(ast, c.float(), s.float(), enc_sd, dec_sd, ada_sd, hip_device)
     with torch.no_grad():
         y2 = ast(c.to(hip_device), s.to(hip_device))
         y1 = ast(c[1:].to(hip_device), s[1:].to(hip_device))
