@@ -25,6 +25,7 @@ SIGNATURES = {
     "ast_version": (ctypes.c_char_p, []),
     "ast_conv3x3_packed_numel": (ctypes.c_size_t, [_i, _i]),
     "ast_conv3x3_pack_weights_f32": (_i, [_p, _p, _i, _i, _p]),
+    "ast_conv3x3_pack_split_f32": (_i, [_p, _i, _i, _p]),
     "ast_conv3x3_fwd_f32": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
     "ast_conv3x3_num_configs": (_i, []),
     "ast_conv3x3_fwd_f32_cfg": (_i, [_i, _p, _p, _i, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),

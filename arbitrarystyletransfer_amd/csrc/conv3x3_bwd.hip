@@ -568,7 +568,8 @@ int ast_conv3x3_pack_weights_ex_f32(const float* w, float* w_packed, int cout, i
   const int pad_out = round_up(cin, 64), pad_in = round_up(cout, 8);
   hipLaunchKernelGGL(pack_tf_kernel, dim3(grid1((int64_t)pad_in * 9 * pad_out)), dim3(256), 0, (hipStream_t)stream,
                      w, w_packed, cout, cin, pad_out, pad_in, in_scale);
-  return (int)hipGetLastError();
+  const int e = (int)hipGetLastError();
+  return e ? e : ast_conv3x3_pack_split_f32(w_packed, cin, cout, stream);   // conv with cin' = cout, cout' = cin
 }
 
 int ast_conv_act_backward_f32(const float* pre, const float* g_pre, const float* g_act, const float* g_pool,

@@ -98,6 +98,78 @@ __device__ __forceinline__ bool decode_block(int id, int ntiles, int groups, int
   return tile < ntiles;
 }
 
+// Epilogue of a wave's RM x RN tiles of 32x32 accumulators (A = pixels, B = channels: lane l32 =
+// output channel n0c + 32j + l32, register 4g + r = pixel x0 + 8g + 4h + r of row y0 + row0 + i):
+// +bias, pre-ReLU / ReLU float4 stores, fused 2x2 max-pool (a lane holds both rows of a window).
+template <int RM, int RN>
+__device__ __forceinline__ void store_tiles(const ConvArgs& a, const f32x16 (&acc)[RM][RN], int n, int x0, int y0,
+                                            int row0, int n0c, int h, int l32) {
+  const int H = a.H, W = a.W;
+  const int64_t plane = (int64_t)H * W;
+  const bool vec4 = (W & 3) == 0;
+  const int Ho = H >> 1, Wo = W >> 1;
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int co = n0c + j * 32 + l32;
+    const bool cok = co < a.Cout;
+    const float bv = (cok && a.bias) ? a.bias[co] : 0.f;
+    const int64_t obase = ((int64_t)n * a.Cout + co) * plane;
+    if (a.y_pre || a.y_act) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int yy = y0 + row0 + i;
+        if (!cok || yy >= H) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int xx = x0 + 8 * g + 4 * h;
+          if (xx >= W) continue;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * g + r] + bv;
+          const int64_t off = obase + (int64_t)yy * W + xx;
+          const bool full = vec4 && xx + 3 < W;
+          if (a.y_pre) {
+            if (full) *reinterpret_cast<float4*>(a.y_pre + off) = make_float4(v[0], v[1], v[2], v[3]);
+            else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_pre[off + r] = v[r];
+          }
+          if (a.y_act) {
+            float u[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) u[r] = relu_f(v[r]);
+            if (full) *reinterpret_cast<float4*>(a.y_act + off) = make_float4(u[0], u[1], u[2], u[3]);
+            else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_act[off + r] = u[r];
+          }
+        }
+      }
+    }
+    if (a.y_pool && cok) {
+      const int64_t pbase = ((int64_t)n * a.Cout + co) * Ho * Wo;
+#pragma unroll
+      for (int i = 0; i + 1 < RM; i += 2) {
+        const int py = (y0 + row0 + i) >> 1;
+        if (py >= Ho) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int px = (x0 + 8 * g + 4 * h) >> 1;
+          if (px >= Wo) continue;
+          float m[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            m[r] = max_nan(relu_f(acc[i][j][4 * g + r] + bv), relu_f(acc[i + 1][j][4 * g + r] + bv));
+          const float p0 = max_nan(m[0], m[1]), p1 = max_nan(m[2], m[3]);
+          const int64_t off = pbase + (int64_t)py * Wo + px;
+          if (px + 1 < Wo && (Wo & 1) == 0) {
+            *reinterpret_cast<float2*>(a.y_pool + off) = make_float2(p0, p1);
+          } else {
+            a.y_pool[off] = p0;
+            if (px + 1 < Wo) a.y_pool[off + 1] = p1;
+          }
+        }
+      }
+    }
+  }
+}
+
 template <int WM, int WN, int RM, int RN, int CK, int UP, bool SWAP, bool NORM>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN >= 16 ? 1 : 2) void conv3x3_f32_kernel(ConvArgs a) {
   using C = Cfg<WM, WN, RM, RN, CK, UP>;
@@ -314,7 +386,6 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN >= 16 ? 1 : 2) void conv3x3_f
   // ---------------- epilogue ----------------
   const int H = a.H, W = a.W;
   const int64_t plane = (int64_t)H * W;
-  const bool vec4 = (W & 3) == 0;
   const int Ho = H >> 1, Wo = W >> 1;
   if constexpr (SWAP) {
     // C^T: lane l32 = output column x0+l32, register r = channel (r&3)+8(r>>2)+4h of the
@@ -363,66 +434,253 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN >= 16 ? 1 : 2) void conv3x3_f
     }
     return;
   }
+  store_tiles<RM, RN>(a, acc, n, x0, y0, wm * RM, n0 + wn * RN * 32, h, l32);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Split-bf16 ("bf16x3") implicit GEMM: fp32 accuracy on the bf16 matrix cores.
+//
+// Every fp32 operand is split exactly into three bf16 terms, x = hi + mid + lo (hi = bf16(x),
+// mid = bf16(x - hi), lo = x - hi - mid, which has <= 8 significant bits and so is exact in bf16).
+// The product x*w is the sum of the 9 cross products; the 3 dropped ones (mid*lo, lo*mid, lo*lo) are
+// below 2^-24 |x w|, i.e. under fp32's own rounding of the product. Six v_mfma_f32_32x32x16_bf16
+// (products exact in fp32, fp32 accumulation) therefore give an fp32-accurate conv at 6 x 16 cycles
+// per 32x32x16 block against 8 x 64 cycles (32x32x2 f32) for the same block on the fp32 MFMA:
+// 2.67x the fp32 matrix peak (2.5 PF / 6 = 419 TF of fp32-equivalent work).
+//
+// Layout (16-byte units = 8 bf16 channels):
+//  * LDS activations [plane][h][src row][src col]: h = which 8 of the chunk's 16 input channels.
+//    The A operand of lane l (pixel l&31, channels 8(l>>5)..+7) is one ds_read_b128; 32 lanes read
+//    32 consecutive 16-B units per half -> conflict-free under the b128 lane grouping.
+//  * LDS weights [plane][tap][h][co]: the B operand of lane l (channel l&31) likewise.
+//  * global weight pack (after the fp32 pack, see ast_conv3x3_packed_numel):
+//    [chunk of 16 ci][plane][tap][h][cout_pad][8] bf16, so a chunk's slab rows are contiguous.
+// The source tile (with halo, zero / reflect padding and the x2 nearest upsample resolved per
+// pixel, as in the fp32 kernel) is gathered with dword loads coalesced along x, split on the VALU
+// and written once per chunk; the next chunk's loads are in flight during the MFMAs.
+// ------------------------------------------------------------------------------------------------
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 struct defeats SROA: scratch)
+
+constexpr int kX3K = 16;  // input channels per chunk (= the MFMA K)
+
+__host__ __device__ constexpr int64_t x3_split_offset(int cin, int cout) {  // floats before the split part
+  return (int64_t)((cin + 7) / 8 * 8) * 9 * ((cout + 63) / 64 * 64);
+}
+
+__device__ __forceinline__ void split3(float x, bf16& hi, bf16& mid, bf16& lo) {
+  hi = (bf16)x;
+  float r = x - (float)hi;
+  if (!(fabsf(x) <= 3.402823466e38f)) r = 0.f;  // inf / NaN: carried by hi alone (torch's inf*w)
+  mid = (bf16)r;
+  lo = (bf16)(r - (float)mid);
+}
+
+// fp32 pack [ci_pad8][9][cout_pad] -> split pack [ci16 chunk][plane][tap][h][cout_pad][8]
+__global__ void pack_x3_kernel(const float* __restrict__ wp, bf16* __restrict__ ws, int cin_pad8, int cin16,
+                               int cout_pad) {
+  const int64_t total = (int64_t)cin16 * 9 * cout_pad;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(idx % cout_pad);
+    const int64_t rt = idx / cout_pad;
+    const int tap = (int)(rt % 9);
+    const int ci = (int)(rt / 9);
+    const float v = ci < cin_pad8 ? wp[((int64_t)ci * 9 + tap) * cout_pad + co] : 0.f;
+    bf16 t[3];
+    split3(v, t[0], t[1], t[2]);
+    const int kc = ci / kX3K, hh = (ci >> 3) & 1, e = ci & 7;
 #pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    const int co = n0 + (wn * RN + j) * 32 + l32;
-    const bool cok = co < a.Cout;
-    const float bv = (cok && a.bias) ? a.bias[co] : 0.f;
-    const int64_t obase = ((int64_t)n * a.Cout + co) * plane;
-    if (a.y_pre || a.y_act) {
+    for (int p = 0; p < 3; ++p)
+      ws[((((int64_t)(kc * 3 + p) * 9 + tap) * 2 + hh) * cout_pad + co) * 8 + e] = t[p];
+  }
+}
+
+template <int WM, int RM, int RN, int UP>
+struct X3Cfg {
+  static constexpr int NT = WM * 64;
+  static constexpr int TH = WM * RM;                 // output rows per tile
+  static constexpr int BN = RN * 32;                 // output channels per tile
+  static constexpr int SR = TH / UP + 2;             // source rows incl. halo
+  static constexpr int SC = TW / UP + 2;             // source columns incl. halo
+  static constexpr int A_PLANE = 2 * SR * SC;        // 16-B units per plane
+  static constexpr int A_UNITS = 3 * A_PLANE;
+  static constexpr int B_ROWS = 3 * 9 * 2;           // (plane, tap, h)
+  static constexpr int B_UNITS = B_ROWS * BN;
+  static constexpr int A_T = (A_PLANE + NT - 1) / NT;  // gather items per thread (one item = 8 channels)
+  static constexpr int B_T = (B_UNITS + NT - 1) / NT;
+  static constexpr int NS = UP == 1 ? RM + 2 : RM / 2 + 2;  // source rows a wave's RM output rows read
+  static constexpr int LDS_BYTES = (A_UNITS + B_UNITS) * 16;
+};
+
+// source row (relative to the wave's first) of output row i at tap row ky
+template <int UP>
+__host__ __device__ constexpr int x3_srel(int i, int ky) { return UP == 1 ? i + ky : ((i + ky - 1) >> 1) + 1; }
+
+template <int WM, int RM, int RN, int UP, int OCC>
+__global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
+  using C = X3Cfg<WM, RM, RN, UP>;
+  constexpr int NT = C::NT, TH = C::TH, BN = C::BN, SR = C::SR, SC = C::SC, A_PLANE = C::A_PLANE;
+  constexpr int A_T = C::A_T, B_T = C::B_T, NS = C::NS;
+  static_assert(RM % 2 == 0, "even rows per wave (pool windows, upsample row pairs)");
+  extern __shared__ __attribute__((aligned(16))) u32x4 x3_smem[];
+  u32x4* As = x3_smem;
+  u32x4* Bs = x3_smem + C::A_UNITS;
+
+  const int tid = threadIdx.x, wm = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  int t, grp;
+  if (!decode_block(blockIdx.x, a.tiles_x * a.tiles_y * a.N, (a.Cout + BN - 1) / BN, t, grp)) return;
+  const int tx = t % a.tiles_x;
+  t /= a.tiles_x;
+  const int ty = t % a.tiles_y;
+  const int n = t / a.tiles_y;
+  const int x0 = tx * TW, y0 = ty * TH;
+  const int sx0 = x0 / UP, sy0 = y0 / UP - 1;
+  const int n0 = grp * BN;
+  const int Hin = a.Hin, Win = a.Win, plane_in = Hin * Win;
+  const float* __restrict__ xin =
+      n < a.nsplit ? a.x + (int64_t)n * a.Cin * plane_in : a.x2 + (int64_t)(n - a.nsplit) * a.Cin * plane_in;
+  const u32x4* __restrict__ wsplit =
+      reinterpret_cast<const u32x4*>(a.wp + x3_split_offset(a.Cin, a.Cout));
+  const int nch = (a.Cin + kX3K - 1) / kX3K;
+  const int64_t chunk_units = (int64_t)C::B_ROWS * a.cout_pad;
+
+  // gather items: (h, source row, source column), fixed per thread for every chunk. Loads are
+  // raw buffer loads: per-chunk descriptor (wave-uniform), per-item 32-bit voffset (pixel + 8h
+  // channels), channel j in soffset: no per-load address arithmetic. A zero-padding pixel gets an
+  // out-of-range voffset, which the buffer range check turns into 0.
+  unsigned g_off[A_T], g_pix[A_T];
+  int g_lds[A_T], g_h[A_T];
+  bool g_ok[A_T];
 #pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        const int yy = y0 + wm * RM + i;
-        if (!cok || yy >= H) continue;
+  for (int i = 0; i < A_T; ++i) {
+    const int e = min(tid + i * NT, A_PLANE - 1);
+    const int c = e % SC, rest = e / SC, r = rest % SR, hh = rest / SR;
+    const int sy = src_index<UP>(sy0 + r, Hin, a.reflect), sx = src_index<UP>(sx0 - 1 + c, Win, a.reflect);
+    g_ok[i] = sy >= 0 && sx >= 0;
+    g_pix[i] = (unsigned)(max(sy, 0) * Win + max(sx, 0));
+    g_off[i] = g_ok[i] ? 4u * (unsigned)(8 * hh * plane_in) + 4u * g_pix[i] : 0x7ffffff0u;
+    g_lds[i] = e;
+    g_h[i] = hh;
+  }
+  const int plane_b = 4 * plane_in;
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<u32x4*>(wsplit), 0, (int)min<int64_t>(0x7fffffff, (int64_t)nch * chunk_units * 16), 0x00020000);
+  int b_src[B_T], b_dst[B_T];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int xx = x0 + 8 * g + 4 * h;
-          if (xx >= W) continue;
-          float v[4];
+  for (int i = 0; i < B_T; ++i) {
+    const int u = min(tid + i * NT, C::B_UNITS - 1), row = u / BN, j = u - row * BN;
+    b_src[i] = 16 * (row * a.cout_pad + n0 + j);
+    b_dst[i] = u;
+  }
+  float ra[A_T][8];
+  u32x4 rb[B_T];
+  // channel ci0 + 8h + j of item i; a partial last chunk clamps the channel (values masked at store)
+#define X3_LOAD(KC)                                                                                     \
+  {                                                                                                     \
+    const int ci0 = (KC) * kX3K;                                                                        \
+    if (ci0 + kX3K <= a.Cin) {                                                                          \
+      const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(                              \
+          const_cast<float*>(xin + (int64_t)ci0 * plane_in), 0, kX3K * plane_b, 0x00020000);           \
+      _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                     \
+        _Pragma("unroll") for (int i = 0; i < A_T; ++i)                                                 \
+          ra[i][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)g_off[i], j * plane_b, 0)); \
+    } else {                                                                                            \
+      _Pragma("unroll") for (int i = 0; i < A_T; ++i)                                                   \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                   \
+          ra[i][j] = xin[(int64_t)min(ci0 + 8 * g_h[i] + j, a.Cin - 1) * plane_in + g_pix[i]];          \
+    }                                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < B_T; ++i)                                                     \
+      rb[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, b_src[i], (int)((KC) * chunk_units * 16), 0)); \
+  }
+#define X3_STORE(KC)                                                                                    \
+  {                                                                                                     \
+    _Pragma("unroll") for (int i = 0; i < A_T; ++i) {                                                   \
+      if (tid + i * NT < A_PLANE) {                                                                     \
+        if ((KC) * kX3K + kX3K > a.Cin) { /* partial last chunk: padding and channels past Cin */        \
+          const int cn = a.Cin - (KC) * kX3K - 8 * g_h[i];                                              \
+          _Pragma("unroll") for (int j = 0; j < 8; ++j) ra[i][j] = (g_ok[i] && j < cn) ? ra[i][j] : 0.f; \
+        }                                                                                               \
+        bf16x8 pv[3];                                                                                   \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                 \
+          bf16 t0, t1, t2;                                                                              \
+          split3(ra[i][j], t0, t1, t2);                                                                 \
+          pv[0][j] = t0;                                                                                \
+          pv[1][j] = t1;                                                                                \
+          pv[2][j] = t2;                                                                                \
+        }                                                                                               \
+        _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                   \
+          As[p * A_PLANE + g_lds[i]] = __builtin_bit_cast(u32x4, pv[p]);                                \
+      }                                                                                                 \
+    }                                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < B_T; ++i)                                                     \
+      if (tid + i * NT < C::B_UNITS) Bs[b_dst[i]] = rb[i];                                              \
+  }
+
+  f32x16 acc[RM][RN];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * g + r] + bv;
-          const int64_t off = obase + (int64_t)yy * W + xx;
-          const bool full = vec4 && xx + 3 < W;
-          if (a.y_pre) {
-            if (full) *reinterpret_cast<float4*>(a.y_pre + off) = make_float4(v[0], v[1], v[2], v[3]);
-            else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_pre[off + r] = v[r];
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  int acol[3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) acol[kx] = ((x0 + l32 + kx - 1) >> (UP - 1)) - sx0 + 1;
+  const int srow0 = wm * RM / UP;
+
+  X3_LOAD(0);
+  X3_STORE(0);
+  __syncthreads();
+  for (int kc = 0; kc < nch; ++kc) {
+    if (kc + 1 < nch) X3_LOAD(kc + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      bf16x8 bfr[3][RN][3];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            bfr[ky][j][p] = __builtin_bit_cast(bf16x8, Bs[((p * 9 + ky * 3 + kx) * 2 + h) * BN + j * 32 + l32]);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        bf16x8 af[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          af[p] = __builtin_bit_cast(bf16x8, As[p * A_PLANE + (h * SR + srow0 + s) * SC + acol[kx]]);
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            if (x3_srel<UP>(i, ky) != s) continue;
+#pragma unroll
+            for (int j = 0; j < RN; ++j) {
+              f32x16 c = acc[i][j];
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[ky][j][0], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[ky][j][2], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[ky][j][1], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[ky][j][0], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[ky][j][1], c, 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[ky][j][0], c, 0, 0, 0);
+            }
           }
-          if (a.y_act) {
-            float u[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) u[r] = relu_f(v[r]);
-            if (full) *reinterpret_cast<float4*>(a.y_act + off) = make_float4(u[0], u[1], u[2], u[3]);
-            else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_act[off + r] = u[r];
-          }
-        }
       }
     }
-    if (a.y_pool && cok) {
-      const int64_t pbase = ((int64_t)n * a.Cout + co) * Ho * Wo;
-#pragma unroll
-      for (int i = 0; i + 1 < RM; i += 2) {
-        const int py = (y0 + wm * RM + i) >> 1;
-        if (py >= Ho) continue;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int px = (x0 + 8 * g + 4 * h) >> 1;
-          if (px >= Wo) continue;
-          float m[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            m[r] = max_nan(relu_f(acc[i][j][4 * g + r] + bv), relu_f(acc[i + 1][j][4 * g + r] + bv));
-          const float p0 = max_nan(m[0], m[1]), p1 = max_nan(m[2], m[3]);
-          const int64_t off = pbase + (int64_t)py * Wo + px;
-          if (px + 1 < Wo && (Wo & 1) == 0) {
-            *reinterpret_cast<float2*>(a.y_pool + off) = make_float2(p0, p1);
-          } else {
-            a.y_pool[off] = p0;
-            if (px + 1 < Wo) a.y_pool[off + 1] = p1;
-          }
-        }
-      }
+    __builtin_amdgcn_sched_barrier(0);
+    if (kc + 1 < nch) {
+      __syncthreads();  // every wave is done reading this chunk
+      X3_STORE(kc + 1);
+      __syncthreads();
     }
   }
+#undef X3_LOAD
+#undef X3_STORE
+  store_tiles<RM, RN>(a, acc, n, x0, y0, wm * RM, n0, h, l32);
 }
 
 // Direct (VALU) 3x3 conv for cout <= 4 — the decoder's final 64->3 conv (models.py:627). As a
@@ -778,6 +1036,34 @@ int launch_cin4(const ConvArgs& a0, hipStream_t s, int up) {
   return (int)hipGetLastError();
 }
 
+template <int WM, int RM, int RN, int UP, int OCC>
+int launch_x3_one(const ConvArgs& a0, hipStream_t s) {
+  using C = X3Cfg<WM, RM, RN, UP>;
+  ConvArgs a = a0;
+  a.tiles_x = cdiv(a.W, TW);
+  a.tiles_y = cdiv(a.H, C::TH);
+  if (cdiv(a.Cout, C::BN) * C::BN > a.cout_pad) return AST_E_UNSUPPORTED;
+  const int64_t ntiles = (int64_t)a.tiles_x * a.tiles_y * a.N;
+  const int64_t nblk = (ntiles + 7) / 8 * 8 * cdiv(a.Cout, C::BN);
+  if (nblk >= 0x7fffffff) return AST_E_SHAPE;
+  auto kern = conv3x3_x3_kernel<WM, RM, RN, UP, OCC>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(C::NT), C::LDS_BYTES, s, a);
+  return (int)hipGetLastError();
+}
+
+// split-bf16 MFMA kernel: no fused input normalisation (conv_1 runs the direct cin<=4 kernel)
+template <int WM, int RM, int RN, int OCC = 1>
+int launch_x3(const ConvArgs& a, hipStream_t s, int up) {
+  if (a.in_mean) return AST_E_UNSUPPORTED;
+  if ((int64_t)a.Cin * a.Hin * a.Win * 4 >= ((int64_t)1 << 31)) return AST_E_UNSUPPORTED;  // 32-bit buffer offsets
+  return up == 2 ? launch_x3_one<WM, RM, RN, 2, OCC>(a, s) : launch_x3_one<WM, RM, RN, 1, OCC>(a, s);
+}
+
 struct CfgEntry {
   int (*fn)(const ConvArgs&, hipStream_t, int);
   int bn;        // output channels per workgroup (weight-slab width)
@@ -813,13 +1099,24 @@ const CfgEntry kConfigs[] = {
     {launch_cin4<4, false>, 64, 4, 1, 0},               // 21: as 18, 4-row tiles
     {launch_cin4<16, true>, 64, 16, 1, 0},              // 22: 16-row tiles, nontemporal stores
     {launch_cin4<32, true>, 64, 32, 1, 0},              // 23: 32-row tiles, nontemporal stores
+    // split-bf16 (fp32-accurate) MFMA implicit GEMM
+    {launch_x3<8, 2, 2>, 64, 16, 2, 0},                 // 24: 16x32 px x 64 ch, 8 waves
+    {launch_x3<4, 2, 2>, 64, 8, 2, 0},                  // 25: 8x32 px x 64 ch, 4 waves
+    {launch_x3<4, 2, 1, 2>, 32, 8, 2, 0},               // 26: 8x32 px x 32 ch, 4 waves, 2 workgroups/CU
+    {launch_x3<8, 2, 1, 1>, 32, 16, 2, 0},              // 27: 16x32 px x 32 ch, 8 waves
 };
 constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
-int auto_config(int cin, int cout, int n, int h, int w, int up, bool pool) {
+int auto_config(int cin, int cout, int n, int h, int w, int up, bool pool, bool norm) {
   if (cout <= 3) return 10;
   if (cout <= 4) return 11;
   if (cin <= 4 && up == 1 && !pool) return 20;  // direct conv: image-input convs (conv_1)
+  if (cin >= kX3K && !norm && (long)cin * (h / up) * (w / up) * 4 < (1L << 31)) {
+    // split-bf16 MFMA (fp32-accurate, 2.67x the fp32 matrix rate): 8x32 px x 32 ch tiles, two
+    // workgroups per CU; upsampled convs the 16-row tile (profiles/r02_conv_cfgs.log)
+    const long t16 = (long)n * cdiv(h, 16) * cdiv(w, 32) * cdiv(cout, 32);
+    return (up == 2 && t16 >= 512) ? 27 : 26;
+  }
   // 16x32 px x 64 ch, 8 waves: fastest on every VGG shape measured (profiles/, conv_tuning.json);
   // the 4-wave 8x32 tile when that leaves too few workgroups to fill 256 CUs.
   const long tiles = (long)n * cdiv(h, 16) * cdiv(w, 32) * cdiv(cout, 64);
@@ -834,7 +1131,21 @@ const char* ast_version(void) { return "ast_hip 0.1 gfx950"; }
 
 size_t ast_conv3x3_packed_numel(int cout, int cin) {
   if (cout <= 0 || cin <= 0) return 0;
-  return (size_t)round_up(cin, kCinAlign) * 9 * (size_t)round_up(cout, kCoutAlign);
+  const size_t cout_pad = (size_t)round_up(cout, kCoutAlign);
+  // fp32 pack [cin_pad8][9][cout_pad], then the split-bf16 pack [cin_pad16][9][cout_pad] x 3 bf16
+  return (size_t)round_up(cin, kCinAlign) * 9 * cout_pad + (size_t)round_up(cin, kX3K) * 9 * cout_pad * 3 / 2;
+}
+
+int ast_conv3x3_pack_split_f32(float* w_packed, int cout, int cin, void* stream) {
+  if (!w_packed) return AST_E_NULLPTR;
+  if (cout <= 0 || cin <= 0) return AST_E_SHAPE;
+  const int cout_pad = round_up(cout, kCoutAlign);
+  const int64_t total = (int64_t)round_up(cin, kX3K) * 9 * cout_pad;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(pack_x3_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w_packed,
+                     reinterpret_cast<bf16*>(w_packed + x3_split_offset(cin, cout)), round_up(cin, kCinAlign),
+                     round_up(cin, kX3K), cout_pad);
+  return (int)hipGetLastError();
 }
 
 int ast_conv3x3_pack_weights_f32(const float* w, float* w_packed, int cout, int cin, void* stream) {
@@ -845,7 +1156,8 @@ int ast_conv3x3_pack_weights_f32(const float* w, float* w_packed, int cout, int 
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(pack_weights_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, w_packed, cout, cin,
                      cout_pad, cin_pad);
-  return (int)hipGetLastError();
+  const int e = (int)hipGetLastError();
+  return e ? e : ast_conv3x3_pack_split_f32(w_packed, cout, cin, stream);
 }
 
 int ast_conv3x3_num_configs(void) { return kNumConfigs; }
@@ -865,7 +1177,7 @@ int ast_conv3x3_fwd_f32_cfg(int cfg, const float* x, const float* x2, int n2, co
   if (pad_mode == 1 && (H < 2 || W < 2)) return AST_E_SHAPE;  // ReflectionPad2d(1) needs size >= 2
   if ((int64_t)cin * h_in * w_in >= ((int64_t)1 << 31)) return AST_E_SHAPE;         // per-image offsets are 32-bit
   if ((int64_t)round_up(cin, kCinAlign) * 9 * round_up(cout, kCoutAlign) >= ((int64_t)1 << 31)) return AST_E_SHAPE;
-  if (cfg < 0) cfg = auto_config(cin, cout, n + n2, H, W, upsample, y_pool != nullptr);
+  if (cfg < 0) cfg = auto_config(cin, cout, n + n2, H, W, upsample, y_pool != nullptr, in_mean != nullptr);
   if (cfg >= kNumConfigs) return AST_E_UNSUPPORTED;
   const CfgEntry& e = kConfigs[cfg];
   if (y_pool && (e.rm % 2 != 0 || e.max_cout)) return AST_E_UNSUPPORTED;

@@ -37,8 +37,13 @@ const char* ast_version(void);
 /* Number of floats of the packed weight buffer for a [cout, cin, 3, 3] filter bank. */
 size_t ast_conv3x3_packed_numel(int cout, int cin);
 
-/* Repack w[cout][cin][3][3] into the kernel layout (zero padded). */
+/* Repack w[cout][cin][3][3] into the kernel layout (zero padded). The packed buffer holds the
+ * fp32 pack [cin_pad8][9][cout_pad64] followed by the split-bf16 pack of the same weights (three
+ * bf16 terms per value, w = hi + mid + lo exactly) that the fp32-accurate bf16-MFMA kernel reads. */
 int ast_conv3x3_pack_weights_f32(const float* w, float* w_packed, int cout, int cin, void* stream);
+
+/* (Re)build the split-bf16 part of a packed buffer from its fp32 part (the pack functions call it). */
+int ast_conv3x3_pack_split_f32(float* w_packed, int cout, int cin, void* stream);
 
 /* y = conv3x3(pad(upsample(x))) + bias, with fused epilogue stores.
  *   x        [n, cin, h_in, w_in]; output spatial size h = h_in*upsample, w = w_in*upsample

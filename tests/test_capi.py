@@ -48,10 +48,11 @@ def test_version_and_configs():
 
 def test_packed_numel():
     L = _lib.lib()
-    # cin padded to 8, cout padded to 64
-    assert L.ast_conv3x3_packed_numel(64, 3) == 8 * 9 * 64
-    assert L.ast_conv3x3_packed_numel(3, 64) == 64 * 9 * 64
-    assert L.ast_conv3x3_packed_numel(512, 256) == 256 * 9 * 512
+    # fp32 pack: cin padded to 8, cout padded to 64; then the split-bf16 pack: cin padded to 16,
+    # three bf16 per weight (1.5 floats)
+    assert L.ast_conv3x3_packed_numel(64, 3) == 8 * 9 * 64 + 16 * 9 * 64 * 3 // 2
+    assert L.ast_conv3x3_packed_numel(3, 64) == 64 * 9 * 64 + 64 * 9 * 64 * 3 // 2
+    assert L.ast_conv3x3_packed_numel(512, 256) == 256 * 9 * 512 + 256 * 9 * 512 * 3 // 2
     assert L.ast_conv3x3_packed_numel(0, 3) == 0
 
 
