@@ -546,6 +546,217 @@ __global__ __launch_bounds__(256, 2) void wgrad2_kernel(WgArgs a) {
 #undef WG2_HALO
 }
 
+// Split-bf16 weight gradient (fp32-accurate on the bf16 matrix cores; the x = hi + mid + lo split and
+// the 6-product sum of conv3x3_igemm.hip's x3 kernel). dW[co][ci][tap] = sum_pix dY[co][pix] *
+// X[ci][pix + tap] as a GEMM with K = pixels, v_mfma_f32_32x32x16_bf16:
+//  * A = dY (rows co): LDS [plane][co][pixel] (row pitch 144 B: conflict-free ds_read_b128 of 8
+//    consecutive pixels per lane);
+//  * B = X shifted by the tap (cols ci): LDS [plane][ci half][halo pixel][32 ci] (64-B rows), read
+//    with ds_read_b64_tr_b16 -- a lane supplies the address of ITS pixel row, so the tap shift, the
+//    zero/reflect padding and the nearest x2 upsample are all just row addresses, at any alignment.
+// A workgroup (4 waves, 2 x 2 over co x ci) owns 64 co x 64 ci x 9 taps (each wave 32 x 32 x 9 in 9
+// accumulators) and sweeps a range of 2 x 32-pixel tiles; ~80 KB LDS: two workgroups per CU, so
+// one's staging (global loads, split, LDS writes) overlaps the other's MFMAs. Partial dW and db meet
+// through fp32 atomics, as in wgrad2_kernel.
+typedef __bf16 bf16_t;
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void wg_split3(float x, bf16_t& hi, bf16_t& mid, bf16_t& lo) {
+  hi = (bf16_t)x;
+  float r = x - (float)hi;
+  if (!(fabsf(x) <= 3.402823466e38f)) r = 0.f;
+  mid = (bf16_t)r;
+  lo = (bf16_t)(r - (float)mid);
+}
+
+template <int UP>
+struct Wg3Cfg {
+  static constexpr int SR = WG_TH / UP + 2, SC = WG_TW / UP + 2;
+  static constexpr int NPIX = SR * SC;                       // halo pixels
+  static constexpr int XROW = 64;                            // bytes per halo pixel row (32 ci)
+  static constexpr int XHALF = NPIX * XROW;                  // bytes per ci half
+  static constexpr int XPLANE = 2 * XHALF;
+  static constexpr int DP = 144;                             // dY row pitch (bytes): 64 px + 8 pad
+  static constexpr int DPLANE = WG_CO * DP;
+  static constexpr int DOFF = 3 * XPLANE;                    // dY image after the X image
+  static constexpr int LDS = 3 * XPLANE + 3 * DPLANE;
+  static constexpr int XI = NPIX * 4;                        // X items per ci half: (pixel, 8-channel group)
+  static constexpr int XT = (XI + 255) / 256;
+};
+
+template <int UP>
+__global__ __launch_bounds__(256, 2) void wgrad3_kernel(WgArgs a) {
+  using C = Wg3Cfg<UP>;
+  constexpr int SC = C::SC, NPIX = C::NPIX, XT = C::XT;
+  extern __shared__ __attribute__((aligned(16))) unsigned char wg3_smem[];
+  const int Hin = a.Hin, Win = a.Win, plane_in = Hin * Win;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int wco = wave & 1, wci = wave >> 1;
+  const int co_groups = a.Cout / WG_CO, ci_groups = a.Cin / WG_CI;
+  int b = blockIdx.x;
+  const int cog = b % co_groups;
+  b /= co_groups;
+  const int cig = b % ci_groups;
+  const int split = b / ci_groups;
+  const int co0 = cog * WG_CO, ci0 = cig * WG_CI;
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = (f32x16){0.f};
+  float bacc[2] = {0.f, 0.f};
+
+  // X staging items: e = tid + 256k -> pixel p = e % NPIX (lanes run along pixels: coalesced
+  // loads), channel group g = e / NPIX (8 channels)
+  // dY staging items: e = tid + 256k (k = 0, 1) -> co = e / 8, pixel octet o = e % 8
+  // B operand (tr read) lane roles: q = (lane >> 2) & 3 (row), p = lane & 3 (column quad), cb =
+  // (lane >> 4) & 1 (16-column block)
+  const int trq = (lane >> 2) & 3, trp = lane & 3, trcb = (lane >> 4) & 1;
+  const int xcol_b = wci * C::XHALF + (16 * trcb + 4 * trp) * 2;  // byte offset of this lane's 4 ci
+  const int arow_b = C::DOFF + (wco * 32 + l32) * C::DP + 16 * h;  // A: co row, pixel octet h of the k-step
+
+  const int t0 = (int)(a.tiles_per_block * split);
+  const int t1 = (int)min(a.ntiles, (int64_t)t0 + a.tiles_per_block);
+  for (int tile = t0; tile < t1; ++tile) {
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int n = tt / a.tiles_y;
+    const int x0 = tx * WG_TW, y0 = ty * WG_TH;
+    const int sx0 = x0 / UP, sy0 = y0 / UP - 1;
+    const float* __restrict__ xin = a.x + ((int64_t)n * a.Cin + ci0) * plane_in;
+    // ---- staging. X is loaded one ci half at a time (registers): half 0 and dY before the barrier
+    // (in flight during the other waves' last MFMAs of the previous tile), half 1 right after it,
+    // in flight while half 0 and dY are split and written ----
+    float xv[XT][8];
+#define WG3_LOAD_X(HALF)                                                                                  \
+    _Pragma("unroll") for (int k = 0; k < XT; ++k) {                                                      \
+      const int e = min(tid + 256 * k, C::XI - 1), p = e % NPIX, g = (HALF) * 4 + e / NPIX;               \
+      const int r = p / SC, c = p % SC;                                                                   \
+      const int sy = src_index<UP>(sy0 + r, Hin, a.reflect), sx = src_index<UP>(sx0 - 1 + c, Win, a.reflect); \
+      const bool ok = sy >= 0 && sx >= 0;                                                                 \
+      const float* src = xin + (int64_t)(8 * g) * plane_in + max(sy, 0) * Win + max(sx, 0);              \
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                     \
+        const float v = src[(int64_t)j * plane_in];                                                       \
+        xv[k][j] = ok ? v : 0.f;                                                                          \
+      }                                                                                                   \
+    }
+#define WG3_STORE_X(HALF)                                                                                 \
+    _Pragma("unroll") for (int k = 0; k < XT; ++k) {                                                      \
+      const int e = tid + 256 * k;                                                                        \
+      if (e < C::XI) {                                                                                    \
+        const int p = e % NPIX, g = (HALF) * 4 + e / NPIX;                                                \
+        bf16x8_t pv[3];                                                                                   \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                   \
+          bf16_t t0_, t1_, t2_;                                                                           \
+          wg_split3(xv[k][j], t0_, t1_, t2_);                                                             \
+          pv[0][j] = t0_;                                                                                 \
+          pv[1][j] = t1_;                                                                                 \
+          pv[2][j] = t2_;                                                                                 \
+        }                                                                                                 \
+        const int off = (g >> 2) * C::XHALF + p * C::XROW + (g & 3) * 16;                                 \
+        _Pragma("unroll") for (int pl = 0; pl < 3; ++pl)                                                  \
+          *reinterpret_cast<u32x4_t*>(wg3_smem + pl * C::XPLANE + off) = __builtin_bit_cast(u32x4_t, pv[pl]); \
+      }                                                                                                   \
+    }
+    WG3_LOAD_X(0)
+    float dv[2][8];
+    const float* __restrict__ dyn = a.dy + (int64_t)n * a.Cout * a.dy_plane + a.dy_off;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + 256 * k, co = e >> 3, o = e & 7;
+      const float* src = dyn + (int64_t)(co0 + co) * a.dy_plane + (int64_t)(y0 + (o >> 2)) * a.dy_pitch + x0 + 8 * (o & 3);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dv[k][j] = src[j];
+    }
+    __syncthreads();  // the previous tile's operand reads are done
+    WG3_STORE_X(0)
+    WG3_LOAD_X(1)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + 256 * k, co = e >> 3, o = e & 7;
+      bf16x8_t pv[3];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bacc[k] += dv[k][j];
+        bf16_t t0_, t1_, t2_;
+        wg_split3(dv[k][j], t0_, t1_, t2_);
+        pv[0][j] = t0_;
+        pv[1][j] = t1_;
+        pv[2][j] = t2_;
+      }
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        *reinterpret_cast<u32x4_t*>(wg3_smem + C::DOFF + pl * C::DPLANE + co * C::DP + 16 * o) =
+            __builtin_bit_cast(u32x4_t, pv[pl]);
+    }
+    WG3_STORE_X(1)
+#undef WG3_LOAD_X
+#undef WG3_STORE_X
+    __syncthreads();
+    // ---- 4 k-steps of 16 pixels: output row pr = ks >> 1, columns 16 (ks & 1) + 0..15 ----
+#pragma unroll 1
+    for (int ks = 0; ks < 4; ++ks) {
+      const int pr = ks >> 1, cj = 16 * (ks & 1);
+      bf16x8_t af[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        af[pl] = *reinterpret_cast<const bf16x8_t*>(wg3_smem + arow_b + pl * C::DPLANE + 32 * ks);
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int srow = (UP == 1) ? pr + ky : ((pr + ky - 1) >> 1) + 1;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          // this lane's rows: k = 8h + 4rr + q of the k-step -> output column cj + k
+          int pix[2];
+#pragma unroll
+          for (int rr = 0; rr < 2; ++rr) {
+            const int xo = cj + 8 * h + 4 * rr + trq;  // output column within the tile
+            const int scol = (UP == 1) ? xo + kx : ((xo + kx - 1) >> 1) + 1;
+            pix[rr] = srow * SC + scol;
+          }
+          bf16x8_t bfr[3];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) {
+            const unsigned char* base = wg3_smem + pl * C::XPLANE + xcol_b;
+            const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + pix[0] * C::XROW));
+            const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + pix[1] * C::XROW));
+            bfr[pl] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          }
+          f32x16 c = acc[ky * 3 + kx];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[1], c, 0, 0, 0);
+          acc[ky * 3 + kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[0], c, 0, 0, 0);
+        }
+      }
+    }
+  }
+  const int ci = ci0 + wci * 32 + l32;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      atomicAdd(a.dw + ((int64_t)co * a.Cin + ci) * 9 + t, acc[t][r]);
+    }
+  if (a.db && cig == 0) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // the 8 threads of one co are 8 consecutive lanes
+      float v = bacc[k];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if ((tid & 7) == 0) atomicAdd(a.db + co0 + ((tid + 256 * k) >> 3), v);
+    }
+  }
+}
+
 int g_wgrad_v1 = 0;  // AST_WGRAD_V1=1: always the general kernel (A/B measurements)
 
 int grid1(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
@@ -676,7 +887,24 @@ int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* 
   const bool aligned = cin % WG_CI == 0 && cout % WG_CO == 0 && W % WG_TW == 0 && H % WG_TH == 0 && w_in % 4 == 0 &&
                        a.ntiles < 0x7fffffff && (int64_t)n * cin * h_in * w_in < 0x7fffffffLL &&
                        (int64_t)cout * dy_plane < 0x7fffffffLL && !g_wgrad_v1;
-  if (aligned && upsample == 2)
+  static const int wver = [] {
+    const char* v = getenv("AST_WGRAD_VERSION");   // 2 = the fp32 MFMA wgrad2 kernel (A/B measurements)
+    return v ? atoi(v) : 3;
+  }();
+  if (aligned && wver >= 3) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)wgrad3_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                Wg3Cfg<1>::LDS);
+      (void)hipFuncSetAttribute((const void*)wgrad3_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                Wg3Cfg<2>::LDS);
+      attr = true;
+    }
+    if (upsample == 2)
+      hipLaunchKernelGGL(wgrad3_kernel<2>, dim3((unsigned)nblk), dim3(256), Wg3Cfg<2>::LDS, s, a);
+    else
+      hipLaunchKernelGGL(wgrad3_kernel<1>, dim3((unsigned)nblk), dim3(256), Wg3Cfg<1>::LDS, s, a);
+  } else if (aligned && upsample == 2)
     hipLaunchKernelGGL(wgrad2_kernel<2>, dim3((unsigned)nblk), dim3(256), WgCfg<2>::LDS, s, a);
   else if (aligned)
     hipLaunchKernelGGL(wgrad2_kernel<1>, dim3((unsigned)nblk), dim3(256), WgCfg<1>::LDS, s, a);

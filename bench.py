@@ -110,8 +110,10 @@ def train_bench(args, dev, rank, world):
                                f"lf+tv{'+hist+org_img+out_of_range' if args.full_losses else ''} losses; "
                                f"clip 2.0 + Adam), bs={B}/GPU {S}x{S} fp32",
                    "global_batch": B * world, "image_size": S, "parallelism": f"data-parallel x{world}"},
-        "roofline": {"bound": "mfma", "kernel": "conv3x3 fwd/dgrad + wgrad MFMA launches of a step",
-                     "achieved": tf, "peak": PEAK_FP32_MFMA_TF, "unit": "TFLOP/s", "frac": tf / PEAK_FP32_MFMA_TF,
+        "roofline": {"bound": "mfma", "kernel": "conv3x3 fwd/dgrad + wgrad MFMA launches of a step (split-bf16)",
+                     "achieved": tf, "peak": PEAK_SPLIT_BF16_TF, "unit": "TFLOP/s", "frac": tf / PEAK_SPLIT_BF16_TF,
+                     "peak_basis": "fp32-accurate ceiling of the split-bf16 kernels: dense bf16 MFMA / 6",
+                     "fp32_mfma_peak": PEAK_FP32_MFMA_TF, "frac_of_fp32_mfma_peak": tf / PEAK_FP32_MFMA_TF,
                      "traffic": None, "wgrad_tflops": wg_tf,
                      "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3),
                      "mfma_tflop_per_step": fl / args.steps / 1e12},

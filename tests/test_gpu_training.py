@@ -39,6 +39,8 @@ ENC_CASES = [
     (1, 16, 16, 32, 64, False, True, False),
     (2, 24, 10, 12, 128, True, True, False),
     (1, 64, 8, 64, 64, True, False, False),
+    (2, 64, 6, 64, 128, True, True, False),   # aligned (Cin, Cout % 64, W % 32): the split-bf16 wgrad3 kernel
+    (1, 128, 4, 32, 64, False, True, False),
 ]
 
 
@@ -100,6 +102,8 @@ DEC_CASES = [
     (2, 64, 6, 32, 64, 1, True),
     (1, 128, 4, 16, 64, 2, True),
     (1, 64, 2, 64, 128, 1, False),
+    (2, 128, 5, 32, 64, 2, True),     # upsampled, odd source rows
+    (1, 64, 16, 64, 64, 1, True),
 ]
 
 
