@@ -62,6 +62,13 @@ SIGNATURES = {
     "ast_mb_pw": (_i, [_i, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _i, _i, _p, _i, _p, _p]),
     "ast_mb_conv3x3_dense": (_i, [_i, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
     "ast_adain_bf16": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _d, _i, _p]),
+    "ast_softmax_rows_f32": (_i, [_p, _ll, _i, _p]),
+    "ast_adaattn_dstats_f32": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
+    "ast_softmax_backward_f32": (_i, [_p, _p, _p, _ll, _i, _p]),
+    "ast_adaattn_square_f32": (_i, [_p, _i, _ll, _p]),
+    "ast_adaattn_dv_f32": (_i, [_p, _p, _p, _i, _ll, _p]),
+    "ast_instance_norm_backward_f32": (_i, [_p, _p, _p, _p, _p, _ll, _ll, _i, _p]),
+    "ast_fma_inplace_f32": (_i, [_p, _p, _p, _ll, _p]),
     "ast_adaattn_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i, _i, _i, _i]),
     "ast_adaattn_fwd": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, ctypes.c_size_t, _i, _i, _i, _i, _i, _i, _p]),
     "ast_soft_hist_f32": (_i, [_p, _i, _ll, _f, _p, _p]),

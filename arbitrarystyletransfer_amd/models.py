@@ -61,8 +61,10 @@ class AdaAttN(nn.Module):
 
     Same module tree as the reference (W_q/W_k/W_v 1x1 convs without bias, att_act, std_act and
     the three parameter-free InstanceNorm2d), so state dicts load unchanged. forward runs
-    ops.adaattn: the Nq x Nk attention matrix is never materialised (one fused HIP kernel).
-    Inference only (it raises under autograd recording rather than silently detaching).
+    ops.adaattn: the Nq x Nk attention matrix is never materialised (one fused HIP kernel). Under
+    autograd (fp32, training the reference's AST, train.py:287-300) the backward recomputes the
+    attention on the MFMA GEMMs (attention.AdaAttNFn) and yields gradients for W_q, W_k, W_v and
+    both inputs.
     """
 
     def __init__(self, inp_size):
@@ -78,12 +80,12 @@ class AdaAttN(nn.Module):
         self.inp_size = inp_size
 
     def forward(self, content_map, style_map):
-        if torch.is_grad_enabled() and (content_map.requires_grad or style_map.requires_grad
-                                        or any(p.requires_grad for p in self.parameters())):
-            raise NotImplementedError("AdaAttN on the HIP path is inference-only: run it under torch.no_grad() "
-                                      "or with frozen parameters and inputs")
         if content_map.shape[1] != self.inp_size:
             raise ops.HipOpError(f"expected {self.inp_size} channels, got {content_map.shape[1]}")
+        if torch.is_grad_enabled() and (content_map.requires_grad or style_map.requires_grad
+                                        or any(p.requires_grad for p in self.parameters())):
+            from . import attention
+            return attention.adaattn(self, content_map, style_map)
         return ops.adaattn(content_map, style_map, self.W_q.weight, self.W_k.weight, self.W_v.weight)
 
 
@@ -487,8 +489,9 @@ class AST(nn.Module):
     (models.py:535-566). `attention=False` (default, the north-star path) stylises each layer with
     AdaIN(content_i, style_i); `attention=True` uses the reference's own choice, AdaAttN modules
     `ada_att_1` / `ada_att_2` (models.py:407-408, 557-558), each over enc_out_channels.
-    Inference only: BN uses running statistics, so the reference's eval()/train() toggling in
-    encode() is not needed.
+    Train mode with autograd (ASTTrainer, train.py:146-300) runs the training kernels: the
+    detached eval-mode encoding of encode(detach=True), AdaAttN / ada_out / decoder with backward,
+    and the train-mode (batch statistics) content encoding feeding org_out, as models.py:425-476.
     """
 
     def __init__(self, style_layers=[4, 7, 10, 12, 16], content_layers=[4, 7, 10, 12, 16], exporting=False,
@@ -526,8 +529,18 @@ class AST(nn.Module):
         return self._adain(content_maps[0], style_maps[0]), self._adain(content_maps[1], style_maps[1])
 
     def encode(self, content_img, style_img, detach=False, return_maps=False):
-        content_maps = self._enc(content_img, out_layers=enc_out_layers)
-        style_maps = self._enc(style_img, out_layers=enc_out_layers)
+        """models.py:535-566. detach=True: the encoder runs in eval mode (running statistics) and its
+        maps are detached (models.py:537-545), so it runs here without recording autograd."""
+        if detach:
+            was = self._enc.training
+            self._enc.eval()
+            with torch.no_grad():
+                content_maps = self._enc(content_img, out_layers=enc_out_layers)
+                style_maps = self._enc(style_img, out_layers=enc_out_layers)
+            self._enc.train(was)
+        else:
+            content_maps = self._enc(content_img, out_layers=enc_out_layers)
+            style_maps = self._enc(style_img, out_layers=enc_out_layers)
         st1, st2 = self.stylize_maps(content_maps, style_maps)
         stylized_map = self.ada_out(st1, st2)
         self._last_content_maps = content_maps
@@ -536,17 +549,27 @@ class AST(nn.Module):
         return stylized_map
 
     def forward(self, content_img, style_img, alpha=1.0):
-        if not self._exporting:
-            t_return, _, t = self.encode(content_img, style_img, detach=True, return_maps=True)
-            c = self._last_content_maps            # == self._enc(content_img, enc_out_layers) in eval mode
-            content_map = self.ada_out(c[0], c[1])
-            if alpha != 1.0:
-                t = alpha * t + (1 - alpha) * content_map
-            org_out = self._dec(content_map)
-        else:
-            t = self.encode(content_img, style_img)
-        self._last_content_maps = None
-        t_cs = self._dec(t)
+        """models.py:425-533: t_cs when exporting, else (t_cs, t_return, org_out).
+
+        t_return = (stylized_map_1, stylized_map_2), the per-layer stylised maps: train.py:276-277
+        pairs t[i] with the stylised image's encoding at each of enc_out_layers, and calc_mean_std
+        asserts 4-D maps (models.py:57), so this is the reading of the unparsable models.py:459
+         under which the reference's training loop runs."""
         if self._exporting:
-            return t_cs
-        return t_cs, t_return, org_out
+            t = self.encode(content_img, style_img)
+            self._last_content_maps = None
+            return self._dec(t)
+        st1, st2, t = self.encode(content_img, style_img, detach=True, return_maps=True)
+        if self.training:
+            # train mode: the content encoding for org_out uses batch statistics (and updates the
+            # running ones), as the reference's second encoder call does (models.py:466-469)
+            c = self._enc(content_img, out_layers=enc_out_layers)
+        else:
+            c = self._last_content_maps    # eval mode: the same maps encode() just computed
+        self._last_content_maps = None
+        content_map = self.ada_out(c[0], c[1])
+        if alpha != 1.0:
+            t = alpha * t + (1 - alpha) * content_map
+        org_out = self._dec(content_map)
+        t_cs = self._dec(t)
+        return t_cs, (st1, st2), org_out

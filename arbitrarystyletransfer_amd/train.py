@@ -40,6 +40,7 @@ import torch.distributed as dist
 from . import dp
 from . import losses as L
 from . import models
+from .conf import enc_out_layers
 from .optim import FusedAdam
 
 STYLE_WEIGHTS = (1.0, 1.0, 1.0, 1.0, 0.75, 0.5)   # train.py:232-238 for the 6 loss-network layers
@@ -174,6 +175,149 @@ class AdaINTrainer:
         d = torch.load(self.save_file, map_location=self.device, weights_only=True)
         self.net.load_state_dict(d["ast"])
         self.optim.load_state_dict(d["ast_optim"])
+        with open(self.train_dict_file) as f:
+            self.train_dict = json.load(f)
+
+
+# ------------------------------------------------------------------------------------------------
+# The reference's own trainer: ASTTrainer (train.py:50-401) over the MobileNet AST with AdaAttN
+# ------------------------------------------------------------------------------------------------
+
+def default_ast_args(**kw):
+    """train.py:405-440 defaults (batch_size, lr and the loss weights)."""
+    a = dict(train_iter=10000, batch_size=8, lr=2e-4, content_lam=1.25, style_lam=0.5, tv_lam=0.0006, lf_lam=1.0,
+             org_img_lam=0.5, save_dir="models/ast/", load=False, ae_model="models/auto_encoder/ae.pth")
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+class ASTTrainer:
+    """ASTTrainer (train.py:50-401) on HIP: models.AST(attention=True) -- MobileNet encoder,
+    AdaAttN at enc_out_layers (ada_att_1 / ada_att_2), ada_out, decoder -- trained end to end in
+    train mode after load_ae (train.py:135-144), every parameter in one Adam (train.py:61).
+
+    Per step (train.py:186-300):
+      stylized, t, org_out = ast(content, style)          (t = the per-layer stylised maps)
+      content/style/t_cs/org_out maps = lossnet(...)      (VGG19 to relu_15, frozen)
+      enc_stylized = ast._enc(stylized)                   (train mode: BN running stats update)
+      content = sum_i huber(mvn(t_cs_map_i), mvn(content_map_i)) + 0.1 huber(mvn(stylized), mvn(content))
+      style   = sum_i w_i style_loss(t_cs_map_i, style_map_i) + style_loss(stylized, style)
+      org_img = org_img_lam (sum_i huber(org_out_map_i, content_map_i) + 100 mean((content - org_out)^2))
+      lf      = sum_i huber(mvn(t_i), mvn(enc_stylized_i))  (gradient into AdaAttN)
+      loss = content_lam content + style_lam style + lf_lam lf + tv_lam tv + 1e-5 hist + org_img + 1e8 out_of_range
+      clip_grad_norm_(2.0, error_if_nonfinite) + Adam(lr, (0.9, 0.999), 1e-5)
+    Data parallel as AdaINTrainer (args.batch_size = global batch, shard-weighted batch-mean terms,
+    one SUM all-reduce of the flat gradient arena) plus SyncBatchNorm for the train-mode encoder."""
+
+    def __init__(self, args=None, device=None, ast=None, lossnet=None, content_iter=None, grad_hook=None):
+        self.args = args or default_ast_args()
+        self.device = torch.device(device or "cuda")
+        self.ast = (ast or models.AST(attention=True)).to(self.device).train()
+        self.pretrained_enc = (lossnet or models.PretrainedEncoder()).to(self.device).eval()
+        self.pretrained_enc.requires_grad_(False)
+        self.content_iter = content_iter
+        if ast is None and not self.args.load and self.args.ae_model and os.path.exists(self.args.ae_model):
+            self.load_ae()
+        self.params = list(self.ast.parameters())
+        self.ast_optim = FusedAdam(self.params, lr=self.args.lr, betas=(0.9, 0.999), eps=1e-5, max_grad_norm=2.0,
+                                   error_if_nonfinite=True)
+        self.grad_hook = grad_hook
+        self.rank, self.world = 0, 1
+        self.grad_arena = None
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            self.rank, self.world = dist.get_rank(), dist.get_world_size()
+            dp.shard_range(self.args.batch_size, self.rank, self.world)
+            dp.convert_sync_batchnorm(self.ast)
+            self.grad_arena = dp.FlatGradArena(self.params, average=False)
+        self.train_dict = {"content_loss": [], "style_loss": [], "lf_loss": [], "tv_loss": [], "org_img_loss": []}
+        self.save_file = os.path.join(self.args.save_dir, "ast.pth")
+        self.train_dict_file = os.path.join(self.args.save_dir, "ast_train_dict.json")
+        if self.args.load:
+            self.load()
+
+    def load_ae(self, path=None):
+        """train.py:135-144: the pretrained AutoEncoder's encoder / ada_out / decoder into the AST."""
+        d = torch.load(path or self.args.ae_model, map_location=self.device, weights_only=True)
+        ae = models.AutoEncoder()
+        ae.load_state_dict(d["AE"])
+        self.ast._enc.load_state_dict(ae.encoder.state_dict())
+        self.ast.ada_out.load_state_dict(ae.ada_out.state_dict())
+        self.ast._dec.load_state_dict(ae.decoder.state_dict())
+
+    def compute_losses(self, content, style):
+        a = self.args
+        b = content.shape[0]
+        stylized, t, org_out = self.ast(content, style)                                 # train.py:191
+        with torch.no_grad():
+            if content.shape == style.shape:                                            # :193-194, one pass
+                both = self.pretrained_enc(content, style)
+                content_map, style_map = [m[:b] for m in both], [m[b:] for m in both]
+            else:
+                content_map, style_map = self.pretrained_enc(content), self.pretrained_enc(style)
+            # :198 (the reference records autograd here but only ever uses the result detached)
+            enc_stylized = self.ast._enc(stylized.detach(), out_layers=enc_out_layers)
+        t_cs_map = self.pretrained_enc(stylized)                                        # :195
+        org_out_map = self.pretrained_enc(org_out)                                      # :196
+        content_terms = [L.content_mvn_loss(x, y) for x, y in zip(t_cs_map, content_map)]              # :217-227
+        content_terms.append(L.content_mvn_loss(stylized, content, 0.1))                               # :258
+        style_terms = [L.style_loss_weighted(x, y, w) for x, y, w in zip(t_cs_map, style_map, STYLE_WEIGHTS)]  # :230-245
+        style_terms.append(L.style_loss_weighted(stylized, style, 1.0))                                # :271
+        org_terms = [L.compute_content_loss(x, y) for x, y in zip(org_out_map, content_map)]           # :248-256
+        org_terms.append(L.pixel_mse_loss(org_out, content, 100.0))                                    # :268
+        content_loss = torch.stack(content_terms).sum()
+        style_loss = torch.stack(style_terms).sum()
+        org_img_loss = torch.stack(org_terms).sum() * a.org_img_lam                                    # :269
+        range_loss = L.out_of_range_loss(stylized, 1e8)                                                # :259
+        hist_loss = L.compute_hist_loss(stylized, style, 1e-5)                                         # :261
+        lf_loss = torch.stack([L.content_mvn_loss(x, y) for x, y in zip(t, enc_stylized)]).sum()       # :275-277
+        tv = L.tv_loss(stylized)                                                                       # :282
+        mean_terms = (a.content_lam * content_loss + a.style_lam * style_loss + a.lf_lam * lf_loss + hist_loss
+                      + org_img_loss + range_loss)
+        loss = mean_terms + a.tv_lam * tv                                                              # :283
+        return {"loss": loss, "_mean_terms": mean_terms, "content_loss": content_loss, "style_loss": style_loss,
+                "lf_loss": lf_loss, "tv_loss": tv, "org_img_loss": org_img_loss, "hist_loss": hist_loss,
+                "out_of_range_loss": range_loss, "stylized": stylized, "t": t, "org_out": org_out}
+
+    def train_step(self, content, style, record=False):
+        out = self.compute_losses(content, style)
+        self.ast_optim.zero_grad(set_to_none=True)                                      # :287
+        if self.world == 1:
+            out["loss"].backward()                                                      # :288
+        else:
+            a, b = dp.shard_range(self.args.batch_size, self.rank, self.world)
+            if content.shape[0] != b - a:
+                raise ValueError(f"rank {self.rank} holds {content.shape[0]} images, its shard is {b - a}")
+            ((b - a) / self.args.batch_size * out["_mean_terms"] + self.args.tv_lam * out["tv_loss"]).backward()
+        if self.grad_arena is not None:
+            self.grad_arena.all_reduce()
+        if self.grad_hook is not None:
+            self.grad_hook(self.params)
+        self.ast_optim.step()                                                           # :292, :300
+        out["grad_norm"] = self.ast_optim.last_grad_norm
+        if record:                                                                      # :302-306
+            for k in ("content_loss", "style_loss", "lf_loss", "tv_loss", "org_img_loss"):
+                self.train_dict[k].append(float(out[k].item()))
+        return out
+
+    def train(self):
+        for cur_iter in range(self.args.train_iter):                                    # :150
+            content, style = next(self.content_iter)
+            self.train_step(content.to(self.device), style.to(self.device), record=True)
+            if (cur_iter + 1) % 32 == 0:                                                # :313
+                self.save()
+
+    def save(self):
+        os.makedirs(self.args.save_dir, exist_ok=True)
+        torch.save({"ast": self.ast.state_dict(), "ast_optim": self.ast_optim.state_dict()}, self.save_file)
+        with open(self.train_dict_file, "w") as f:
+            json.dump(self.train_dict, f)
+
+    def load(self):
+        d = torch.load(self.save_file, map_location=self.device, weights_only=True)
+        self.ast.load_state_dict(d["ast"])
+        self.ast_optim.load_state_dict(d["ast_optim"])
+        for g in self.ast_optim.param_groups:                                           # train.py:94-98
+            g["betas"], g["lr"], g["eps"] = (0.9, 0.999), self.args.lr, 1e-5
         with open(self.train_dict_file) as f:
             self.train_dict = json.load(f)
 

@@ -298,6 +298,31 @@ int ast_adain_bf16(const void* content, const void* style, void* out, int n, int
  * content [n][c][hc][wc], style [n][c][hs][ws], out like content (dtype 0 = fp32);
  * wq/wk/wv [c][c] fp32 (the Conv2d weights [c][c][1][1]). c <= 128.
  * workspace: device scratch of ast_adaattn_workspace_bytes() bytes (Q, K, V, statistics). */
+/* ---------------------------------------------------------------------------------------------
+ * AdaAttN backward stages (csrc/adaattn_bwd.hip; the GEMMs between them are ast_mbt_gemm_f32).
+ * Notation per image: C channels, N content pixels, M style pixels; O = [mean | ex2] [N][2C].
+ * ------------------------------------------------------------------------------------------ */
+/* s[r][:] = softmax(s[r][:]) in place, rows x cols (nn.Softmax(dim=-1), models.py:97-99). */
+int ast_softmax_rows_f32(float* s, long long rows, int cols, void* stream);
+/* From O [n][N][2C], G = dL/dout [n][C][N] and IN(c) [n][C][N]: dO [n][N][2C] (d mean | d ex2 of
+ * out = sqrt(relu(ex2 - mean^2)) IN(c) + mean, models.py:101-115), D[n*N] = rowsum(dO * O) and
+ * optionally std [n][C][N]. */
+int ast_adaattn_dstats_f32(const float* o2, const float* g, const float* chat, float* do2, float* drow,
+                           float* std_out, int n, int c, int npix, void* stream);
+/* dS = P * (dP - D[row]) in place in dp (softmax backward), rows x cols. */
+int ast_softmax_backward_f32(const float* p, float* dp, const float* drow, long long rows, int cols,
+                             void* stream);
+/* vv [n][2][cm]: vv[b][1] = vv[b][0]^2 (the [V; V^2] operand). */
+int ast_adaattn_square_f32(float* vv, int n, long long cm, void* stream);
+/* dv [n][cm] = dvv[b][0] + 2 vv[b][0] * dvv[b][1]. */
+int ast_adaattn_dv_f32(const float* dvv, const float* vv, float* dv, int n, long long cm, void* stream);
+/* InstanceNorm2d backward (no affine) per plane, given the forward's mean / std = sqrt(var + eps)
+ * (biased var): dx (=|+=) (dxh - mean(dxh) - xh mean(dxh xh)) / std. */
+int ast_instance_norm_backward_f32(const float* x, const float* mean, const float* std, const float* dxh,
+                                   float* dx, long long planes, long long hw, int accumulate, void* stream);
+/* dst += a * b elementwise. */
+int ast_fma_inplace_f32(float* dst, const float* a, const float* b, long long n, void* stream);
+
 size_t ast_adaattn_workspace_bytes(int dtype, int n, int c, int hc, int wc, int hs, int ws);
 int ast_adaattn_fwd(int dtype, const void* content, const void* style, const float* wq,
                     const float* wk, const float* wv, void* out, void* workspace,

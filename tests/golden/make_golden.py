@@ -196,6 +196,7 @@ def main():
     mobilenet_golden(R)
     adaattn_golden(R)
     init_golden(R)
+    ast_train_golden(R)
     print("golden vectors written to", HERE)
 
 
@@ -441,6 +442,135 @@ def train_step_golden(R, enc_wb, dec_wb, full=False):
     np.savez_compressed(os.path.join(HERE, "train_step_full_64.npz" if full else "train_step_64.npz"), **out)
 
 
+AST_ATT_SCALE = 0.125   # W_q, W_k scaled after the live init: diffuse attention (see adaattn_golden)
+
+
+AST_SPREAD_EPS = 1e-6  # input perturbation of the conditioning-spread runs
+
+
+def ast_train_golden(R):
+    """The golden ASTTrainer step (_ast_step) plus its conditioning spread: the same step rerun from
+    inputs perturbed by AST_SPREAD_EPS * N(0, 1) (two draws); per gradient tensor the largest
+    max|g' - g| / max(max|g|, 1e-5 * norm) is stored as `spread:<name>`. ReLU / max-pool routing
+    of the loss network and the train-mode BatchNorm statistics move individual gradient tensors
+    by up to a few percent under a 1e-6 input change (ada_out's expand weight: 4e-2), so a fixed
+    per-tensor tolerance would test the rounding of the CPU reference, not the GPU path."""
+    content = torch.from_numpy(synth.image(951, (2, 3, 64, 64)))
+    style = torch.from_numpy(synth.image(952, (2, 3, 64, 64)))
+    out = _ast_step(R, content, style)
+    norm = float(out["grad_norm"])
+    for k in [k for k in out if k.startswith("grad:")]:
+        out["spread:" + k[5:]] = np.array(0.0)
+    for seed in (961, 962):
+        gen = torch.Generator().manual_seed(seed)
+        pc = content + AST_SPREAD_EPS * torch.randn(content.shape, generator=gen)
+        ps = style + AST_SPREAD_EPS * torch.randn(style.shape, generator=gen)
+        alt = _ast_step(R, pc, ps)
+        for k in [k for k in out if k.startswith("grad:")]:
+            ref = out[k]
+            e = np.abs(alt[k] - ref).max() / max(np.abs(ref).max(), 1e-5 * norm)
+            out["spread:" + k[5:]] = np.maximum(out["spread:" + k[5:]], np.array(e))
+        for k in [k for k in out if k.startswith("buf:")]:   # BatchNorm running statistics
+            e = np.abs(alt[k] - out[k]).max() / max(np.abs(out[k]).max(), 1e-30)
+            out["bufspread:" + k[4:]] = np.maximum(out.get("bufspread:" + k[4:], np.array(0.0)), np.array(e))
+    np.savez_compressed(os.path.join(HERE, "ast_train_step_64.npz"), **out)
+
+
+def _ast_step(R, content, style):
+    """One step of the reference's own trainer, ASTTrainer (train.py:186-300), on the reference's
+    modules: Encoder / Decoder / AutoEncoder.ada_out (live init 5/6/7), AdaAttN(128) x 2 (live init
+    8/9, W_q and W_k x AST_ATT_SCALE: the well-conditioned diffuse regime) composed as AST.forward /
+    AST.encode (models.py:425-476, 535-566) with t = (stylized_map_1, stylized_map_2) (the reading
+    under which train.py:276-277 runs; models.py:459 does not parse), every module in train mode;
+    the VGG loss network (live init 1); the losses exactly as train.py:217-283 assembles them;
+    clip_grad_norm_(2.0, error_if_nonfinite) and Adam(2e-4, (0.9, 0.999), 1e-5) over all of them."""
+    L = R["_losses"]
+    mvn = R["mean_variance_norm"]
+    torch.manual_seed(0)
+    enc = synth.live_init_(R["Encoder"](), 5)
+    dec = synth.live_init_(R["Decoder"](), 6)
+    ada_out = synth.live_init_(R["AutoEncoder"]().ada_out, 7)
+    att1 = synth.live_init_(R["AdaAttN"](128), 8)
+    att2 = synth.live_init_(R["AdaAttN"](128), 9)
+    with torch.no_grad():
+        for att in (att1, att2):
+            att.W_q.weight.mul_(AST_ATT_SCALE)
+            att.W_k.weight.mul_(AST_ATT_SCALE)
+    named = [("_enc", enc), ("_dec", dec), ("ada_att_1", att1), ("ada_att_2", att2), ("ada_out", ada_out)]
+    for _, m in named:
+        m.train()
+    lossnet = R["PretrainedEncoder"]().eval()
+    set_convs(lossnet, synth.vgg_encoder_weights(1))
+    for p in lossnet.parameters():
+        p.requires_grad_(False)
+    params = [(f"{pre}.{n}", p) for pre, m in named for n, p in m.named_parameters()]
+    opt = torch.optim.Adam([p for _, p in params], lr=2e-4, betas=[0.9, 0.999], eps=1e-5)
+    layers = [12, 14]                                                                   # conf.py:112
+    # AST.forward -> encode(detach=True) (models.py:535-545): eval-mode encoder, detached maps
+    enc.eval()
+    cm = [m.detach() for m in enc(content, out_layers=layers)]
+    sm = [m.detach() for m in enc(style, out_layers=layers)]
+    enc.train()
+    st1, st2 = att1(cm[0], sm[0]), att2(cm[1], sm[1])                                   # :557-558
+    t_map = ada_out(torch.cat((st1, st2), dim=1))                                       # :563-565
+    c_maps = enc(content, out_layers=layers)                                            # :466-468 (train mode)
+    content_map_ae = ada_out(torch.cat((c_maps[0], c_maps[1]), dim=1))
+    org_out = dec(content_map_ae)                                                       # :474
+    stylized = dec(t_map)                                                               # :506
+    t = (st1, st2)
+    # train.py:193-283
+    content_map = lossnet(content)
+    style_map = lossnet(style)
+    t_cs_map = lossnet(stylized)
+    org_out_map = lossnet(org_out)
+    enc_stylized = enc(stylized, out_layers=layers)
+    for i in range(len(t_cs_map)):
+        term = L.compute_content_loss(mvn(t_cs_map[i]), mvn(content_map[i].detach()))
+        content_loss = term if i == 0 else content_loss + term
+    for i in range(len(t_cs_map)):
+        w = 0.5 if i == len(t_cs_map) - 1 else (0.75 if i == len(t_cs_map) - 2 else 1.0)
+        term = L.compute_style_loss(t_cs_map[i], style_map[i].detach()) * w
+        style_loss = term if i == 0 else style_loss + term
+    for i in range(len(org_out_map)):
+        term = L.compute_content_loss(org_out_map[i], content_map[i].detach())
+        org_img_loss = term if i == 0 else org_img_loss + term
+    content_loss = content_loss + L.compute_content_loss(mvn(stylized), mvn(content)) * 0.1
+    out_of_range_loss = L.compute_content_loss(stylized, torch.clip(stylized.detach(), 0.0, 1.0)) * 1e8
+    hist_loss = L.compute_hist_loss(stylized, style) * 1e-5
+    org_img_loss = (org_img_loss + ((content.detach() - org_out) ** 2).mean() * 100) * 0.5
+    style_loss = style_loss + L.compute_style_loss(stylized, style) * 1.0
+    lf_loss = 0
+    for i in range(len(enc_stylized)):
+        lf_loss = lf_loss + L.compute_content_loss(mvn(t[i]), mvn(enc_stylized[i].detach()))
+    tv = L.tv_loss(stylized)
+    loss = 1.25 * content_loss + 0.5 * style_loss + 1.0 * lf_loss + 0.0006 * tv + hist_loss + org_img_loss \
+        + out_of_range_loss
+    opt.zero_grad()
+    loss.backward()
+    grads = {n: (p.grad.detach().clone() if p.grad is not None else None) for n, p in params}
+    norm = torch.nn.utils.clip_grad_norm_([p for _, p in params], 2.0, error_if_nonfinite=True)
+    opt.step()
+    out = dict(content=content.numpy(), style=style.numpy(), stylized=stylized.detach().numpy(),
+               org_out=org_out.detach().numpy(), t1=st1.detach().numpy(), t2=st2.detach().numpy(),
+               grad_norm=norm.detach().numpy())
+    for k, v in (("content_loss", content_loss), ("style_loss", style_loss), ("lf_loss", lf_loss), ("tv_loss", tv),
+                 ("org_img_loss", org_img_loss), ("hist_loss", hist_loss), ("out_of_range_loss", out_of_range_loss),
+                 ("loss", loss)):
+        out[k] = v.detach().numpy()
+    for n, p in params:
+        g = grads[n]
+        if g is None:
+            out[f"nograd:{n}"] = np.array(1)
+            continue
+        out[f"grad:{n}"] = g.numpy() if g.numel() <= 2048 else g.reshape(-1)[::17].numpy()
+        out[f"param:{n}"] = p.detach().numpy() if p.numel() <= 2048 else p.detach().reshape(-1)[::17].numpy()
+    for pre, m in named:
+        for n, b in m.named_buffers():
+            if "running" in n:
+                out[f"buf:{pre}.{n}"] = b.numpy()
+    return out
+
+
 INIT_BLOCKS = (   # (inp, oup, stride, expand_ratio, kernel_size, use_norm, use_identity)
     (16, 24, 2, 6, 3, True, True),
     (40, 40, 1, 6, 5, True, True),
@@ -474,6 +604,8 @@ def init_golden(R):
 if __name__ == "__main__":
     if "--init" in sys.argv:
         init_golden(load_reference())
+    elif "--ast-train" in sys.argv:
+        ast_train_golden(load_reference())
     elif "--mobilenet" in sys.argv:
         torch.manual_seed(0)
         mobilenet_golden(load_reference())

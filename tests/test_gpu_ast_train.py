@@ -1,0 +1,161 @@
+"""GPU parity of the reference's own trainer (train.py:50-300, ASTTrainer over the MobileNet AST
+with AdaAttN): AdaAttN's HIP backward against CPU autograd of the oracle, and
+one full ASTTrainer step against the golden step the reference's modules and losses produced
+(tests/golden/ast_train_step_64.npz, make_golden.py --ast-train).
+
+Tolerances (written here): AdaAttN gradients rel_inf <= 1e-4 (diffuse attention, fp32; the GEMM
+summation order differs from torch.bmm); the trainer step: loss terms rtol 1e-4, images and
+stylised maps 1e-4, gradient norm rtol 1e-3; each gradient tensor within max(1e-3, 2 x spread) of
+max(max|g|, 1e-5 * norm), where spread is the CPU reference's own movement when its inputs are
+perturbed by 1e-6 (`spread:<name>` in the fixture, make_golden.ast_train_golden: median 9e-3,
+ada_out's expand weight 4e-2 -- ReLU / max-pool routing of the loss network and train-mode
+BatchNorm statistics), and the mean over tensors of err / max(1e-3, spread) <= 1; updated
+parameters as Adam's sign-like first step allows (within 1e-6 wherever |g| is large enough
+that the gradient bound cannot move the step by more).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from arbitrarystyletransfer_amd import models, synth
+from oracle import ref_cpu as R
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ast_train_step_64.npz")
+ATT_SCALE = 0.125   # make_golden.AST_ATT_SCALE: W_q, W_k scaled after the live init (diffuse attention)
+
+
+def rel_inf(a, b):
+    a = np.asarray(a.detach().cpu() if torch.is_tensor(a) else a, np.float64)
+    b = np.asarray(b.detach().cpu() if torch.is_tensor(b) else b, np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+@pytest.mark.parametrize("shape", [((2, 16, 6, 10), (2, 16, 7, 5)), ((1, 128, 16, 12), (1, 128, 9, 20)),
+                                   ((2, 128, 8, 8), (2, 128, 8, 8))])
+def test_adaattn_backward_vs_oracle(shape, hip_device):
+    """dL/d(content, style, W_q, W_k, W_v) of AdaAttN (models.py:81-115) vs torch CPU autograd of
+    the oracle restatement, for a random upstream gradient."""
+    cs, ss = shape
+    C = cs[1]
+    m = synth.live_init_(models.AdaAttN(C), 31 + C)
+    with torch.no_grad():
+        m.W_q.weight.mul_(ATT_SCALE)
+        m.W_k.weight.mul_(ATT_SCALE)
+    c = torch.from_numpy((synth.uniform(41, int(np.prod(cs))) * 1.5 + 0.25).astype(np.float32).reshape(cs))
+    s = torch.from_numpy((synth.uniform(42, int(np.prod(ss))) * 2.0 - 0.5).astype(np.float32).reshape(ss))
+    g = torch.from_numpy((synth.uniform(43, int(np.prod(cs))) - 0.5).astype(np.float32).reshape(cs))
+    w = [m.W_q.weight.detach().clone(), m.W_k.weight.detach().clone(), m.W_v.weight.detach().clone()]
+    cr, sr = c.clone().requires_grad_(), s.clone().requires_grad_()
+    wr = [t.clone().requires_grad_() for t in w]
+    ref = R.adaattn(cr, sr, *wr)
+    (ref * g).sum().backward()
+    md = m.to(hip_device)
+    cd, sd = c.to(hip_device).requires_grad_(), s.to(hip_device).requires_grad_()
+    out = md(cd, sd)
+    assert rel_inf(out, ref) <= 1e-4
+    (out * g.to(hip_device)).sum().backward()
+    for name, got, want in (("content", cd.grad, cr.grad), ("style", sd.grad, sr.grad), ("W_q", md.W_q.weight.grad, wr[0].grad),
+                            ("W_k", md.W_k.weight.grad, wr[1].grad), ("W_v", md.W_v.weight.grad, wr[2].grad)):
+        e = rel_inf(got, want)
+        assert e <= 1e-4, (name, e)
+
+
+def test_ast_trainer_step_golden(hip_device):
+    """One ASTTrainer step (train.py:186-300): forward of the AST in train mode, the four loss-
+    network passes, every loss term, backward through decoder / ada_out / AdaAttN / train-mode
+    encoder, clip 2.0 + Adam over all parameters -- against the reference's own step."""
+    from arbitrarystyletransfer_amd.train import ASTTrainer, default_ast_args
+    g = np.load(GOLDEN)
+    ast = models.AST(attention=True).load_live_init()
+    with torch.no_grad():
+        for att in (ast.ada_att_1, ast.ada_att_2):
+            att.W_q.weight.mul_(ATT_SCALE)
+            att.W_k.weight.mul_(ATT_SCALE)
+    snap, p0 = {}, {}
+
+    def hook(params):
+        for n, p in tr.ast.named_parameters():
+            snap[n] = p.grad.detach().clone()
+            p0[n] = p.detach().clone()
+
+    tr = ASTTrainer(default_ast_args(batch_size=2), device=hip_device, ast=ast, grad_hook=hook)
+    content, style = torch.from_numpy(g["content"]).to(hip_device), torch.from_numpy(g["style"]).to(hip_device)
+    out = tr.train_step(content, style)
+    for k in ("content_loss", "style_loss", "lf_loss", "tv_loss", "org_img_loss", "hist_loss", "out_of_range_loss",
+              "loss"):
+        np.testing.assert_allclose(out[k].item(), float(g[k]), rtol=1e-4, atol=1e-9, err_msg=k)
+    assert rel_inf(out["stylized"], g["stylized"]) <= 1e-4
+    assert rel_inf(out["org_out"], g["org_out"]) <= 1e-4
+    assert rel_inf(out["t"][0], g["t1"]) <= 1e-4 and rel_inf(out["t"][1], g["t2"]) <= 1e-4
+    norm = out["grad_norm"].item()
+    np.testing.assert_allclose(norm, float(g["grad_norm"]), rtol=1e-3)
+    coef = min(1.0, 2.0 / (norm + 1e-6))
+    lr, eps = 2e-4, 1e-5
+
+    def sub(t, ref):
+        t = t.reshape(-1)
+        return (t if t.numel() == ref.size else t[::17]).reshape(ref.shape)
+
+    worst, far, total, rows, ratios = 0.0, 0, 0, [], []
+    for n, p in tr.ast.named_parameters():
+        ref = g[f"grad:{n}"]
+        scale = max(float(np.abs(ref).max()), 1e-5 * norm)
+        spread = float(g[f"spread:{n}"])
+        e = float(np.abs(sub(snap[n], ref).cpu().numpy() - ref).max()) / scale
+        rows.append((e / max(1e-3, 2 * spread), e, n))
+        ratios.append(e / max(1e-3, spread))
+        worst = max(worst, e / max(1e-3, 2 * spread))
+        gc = snap[n] * coef
+        want = p0[n] - lr * gc / (gc.abs() + eps)   # Adam's first step from our own clipped gradient
+        assert rel_inf(p.detach(), want) <= 1e-5, n
+        pref = g[f"param:{n}"]
+        d = np.abs(sub(p.detach(), pref).cpu().numpy() - pref)
+        assert d.max() <= 2.05 * lr, n
+        # Adam's first step is sign-like only where |g coef| >> eps; there an error of at most the
+        # gradient bound (2 spread scale) moves the parameter by lr eps dg / g^2 <= 1e-6
+        dg = 2 * max(1e-3, spread) * scale
+        sure = np.abs(ref) * coef > np.maximum(np.sqrt(lr * eps * dg * coef / 1e-6), 2 * dg * coef)
+        far += int((d[sure] > 1e-6).sum())
+        total += int(sure.sum())
+    mean_ratio = float(np.mean(ratios))
+    print(f"AST step: worst err/bound {worst:.2f} ({sorted(rows)[-1][2]}); mean err/spread {mean_ratio:.2f}; "
+          f"params off by > 1e-6: {far}/{total}")
+    if os.environ.get("AST_GRAD_TABLE"):
+        for r, e, n in sorted(rows)[-25:]:
+            print(f"  {r:.2f} {e:.2e} {n}")
+    assert worst <= 1.0, sorted(rows)[-3:]
+    assert mean_ratio <= 1.0, mean_ratio
+    assert far <= 1e-4 * total, (far, total)
+    # running statistics: rel_inf <= max(1e-4, 2 x the reference's own spread) -- the deep encoder
+    # blocks' statistics come from the train-mode pass over the stylised image (train.py:229)
+    brows = sorted((rel_inf(b, g[f"buf:{n}"]) / max(1e-4, 2 * float(g[f"bufspread:{n}"])), n)
+                   for n, b in tr.ast.named_buffers() if f"buf:{n}" in g.files)
+    print(f"BN running statistics: {len(brows)} buffers, worst err/bound {brows[-1]}")
+    if os.environ.get("AST_GRAD_TABLE"):
+        for e, n in brows[-12:]:
+            print(f"  {e:.2f} {n}")
+    assert len(brows) == 84 and brows[-1][0] <= 1.0, brows[-3:]
+
+
+def test_ast_trainer_checkpoint_roundtrip(tmp_path, hip_device):
+    """ast.pth {"ast", "ast_optim"} + ast_train_dict.json (train.py:103-133), and load_ae
+    (train.py:135-144) from an ae.pth {"AE", "optim"}."""
+    from arbitrarystyletransfer_amd.train import ASTTrainer, default_ast_args
+    ae = models.AutoEncoder().load_live_init()
+    torch.save({"AE": ae.state_dict(), "optim": {}}, tmp_path / "ae.pth")
+    tr = ASTTrainer(default_ast_args(batch_size=1, save_dir=str(tmp_path), ae_model=str(tmp_path / "ae.pth")),
+                    device=hip_device)
+    for a, b in ((tr.ast._enc, ae.encoder), (tr.ast.ada_out, ae.ada_out), (tr.ast._dec, ae.decoder)):
+        for (k, v), (k2, v2) in zip(a.state_dict().items(), b.state_dict().items()):
+            assert k == k2 and torch.equal(v.cpu(), v2)
+    x = torch.from_numpy(synth.image(5, (1, 3, 64, 64))).to(hip_device)
+    tr.train_step(x, x.flip(3).contiguous(), record=True)
+    tr.save()
+    tr2 = ASTTrainer(default_ast_args(batch_size=1, save_dir=str(tmp_path), load=True), device=hip_device)
+    for (k, v), (k2, v2) in zip(tr.ast.state_dict().items(), tr2.ast.state_dict().items()):
+        assert k == k2 and torch.equal(v, v2), k
+    assert tr2.train_dict == tr.train_dict and len(tr2.train_dict["lf_loss"]) == 1
