@@ -92,8 +92,10 @@ def test_adaattn_module_and_guards():
         out = m(x, y)
     ref = R.adaattn(x.cpu(), y.cpu(), m.W_q.weight.cpu(), m.W_k.weight.cpu(), m.W_v.weight.cpu())
     assert rel_inf(out, ref) <= 1e-3
-    with pytest.raises(NotImplementedError):
-        m(x, y)  # parameters require grad and autograd is recording
+    out_g = m(x, y)  # autograd recording: the training path (attention.AdaAttNFn), same forward launch
+    assert out_g.requires_grad and torch.equal(out_g.detach(), out)
+    with pytest.raises(ops.HipOpError):
+        m(x.bfloat16(), y.bfloat16())  # training runs in fp32 (the reference trains in fp32)
     with pytest.raises(ops.HipOpError):
         ops.adaattn(torch.rand(1, 129, 4, 4, device="cuda"), torch.rand(1, 129, 4, 4, device="cuda"),
                     *(torch.rand(129, 129, device="cuda") for _ in range(3)))
