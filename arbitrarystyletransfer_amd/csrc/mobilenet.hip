@@ -9,7 +9,9 @@
 //                      16x16x4) into a 16-channel LDS chunk of the hidden tensor, Hardswish; depthwise
 //                      kxk on VALU from LDS, +bias, Hardswish; writes the dw output D once and adds the
 //                      per-(n, channel) sums that SELayer's AdaptiveAvgPool needs (atomics).
-//                      The expanded hidden tensor never reaches HBM.
+//                      The expanded hidden tensor never reaches HBM. Three generations: v1 (any dtype,
+//                      stride 1/2), v2 (bf16, one barrier per chunk), v3 (bf16, stride 1, expand
+//                      blocks: the depthwise on MFMA in Toeplitz form, parameters resident in LDS).
 //   se_fold_kernel     SE MLP per image (mobilenetv2.py:63-81) and folds the gate into the pw-linear
 //                      weights: Wg[n][co][c] = W2[co][c] * gate[n][c]   (x*gate then conv == conv with Wg).
 //   pw_kernel          per-image GEMM out = Wg[n] . D + b (+ residual, optionally nearest-upsampled),
@@ -745,6 +747,326 @@ __global__ __launch_bounds__(NT_, 4) void expand_dw2_kernel(EdArgs a) {  // 4 wa
 }
 
 // ------------------------------------------------------------------------------------------------
+// expand + depthwise, v3 (bf16, stride 1, expand blocks): the depthwise on MFMA
+// ------------------------------------------------------------------------------------------------
+// The v1/v2 kernels are VALU-issue-bound (PMC, k5 40->240 at 1024^2: 9.7k VALU instructions per
+// wave for 1.9k depthwise FMAs per thread; two waves per SIMD at ~2 cycles each fill the wave
+// lifetime). Here the kxk depthwise of one hidden channel over the 8 x 32 output tile is one set of
+// 16x16x32 bf16 MFMAs (Toeplitz form):
+//   M = output column xout within a 16-column half, N = (output row r, half ct) (16 pairs),
+//   K = (ky, input column xin), 24 columns per ky (k*24 padded to 32-steps: 3 steps k3, 4 steps k5)
+//   D[xout][(r, ct)] = sum_{ky, xin} T[xout][(ky, xin)] * H[r + ky][16 ct + xin]
+//   T[xout][(ky, xin)] = w[ky][xin - xout] if 0 <= xin - xout < k, else 0.
+// The B operand is two 8-byte LDS reads of the hidden image per step. The A operand (Toeplitz, per
+// channel) comes from a small LDS table Z per chunk: for each (channel, ky) the weight row zero-padded
+// (index 15 + kx holds w[ky][kx]) in two copies shifted by one element, so a lane's 8 consecutive
+// entries start on a 4-byte boundary in one of them; windows that hold no weight read a zero block.
+// Layout constants were chosen with a bank model of the gfx950 LDS (b64: 2 x 32-lane groups over 64
+// banks; b32: 32 banks): the Z reads are conflict-free, the H reads within 1.5-2x of ideal.
+// The expand bias is the MFMA accumulator's initial value, as is the depthwise bias. The hidden image
+// is bf16 (v2's convention); all accumulation fp32.
+template <int K, int NT_ = 512>
+struct Ed3Geom {
+  static constexpr int TH = 8, TW = 32, NT = NT_;
+  static constexpr int CPW = 16 / (NT / 64);       // depthwise channels per wave per chunk
+  static constexpr int IH = TH + K - 1, IW = TW + K - 1;
+  static constexpr int IWE = (IW + 3) / 4 * 4;     // halo row length of the expand enumeration (36)
+  static constexpr int NPE = IH * IWE;
+  static constexpr int HP = (NPE + 15) / 16 * 16;  // expand pixels, MFMA tiles of 16
+  static constexpr int NTILE = HP / 16;
+  static constexpr int TPW = (NTILE + NT / 64 - 1) / (NT / 64);  // expand tiles per wave
+  static constexpr int IWP = 44;                   // hidden row pitch (bf16); columns [IWE, 40) stay zero
+  // hidden channel pitch (bf16): room for the last expand tile's overhang past the halo (HP - NPE
+  // elements after row IH-1), and pitch/4 odd so the expand's 8-byte writes (16 lanes = 16 channels)
+  // hit 16 distinct bank pairs
+  static constexpr int CHP0 = IH * IWP + (HP - NPE);
+  static constexpr int CHP = CHP0 + ((CHP0 / 4) % 2 == 0 ? 4 : 8);
+  static constexpr int KSEG = 24;                  // K columns per ky
+  static constexpr int KSTEPS = (K * KSEG + 31) / 32;
+  static constexpr int ZWC = K == 5 ? 9 : 8;       // words per shifted copy
+  static constexpr int ZROW = K == 5 ? 21 : 17;    // words per (channel, ky)
+  static constexpr int ZZERO = K == 5 ? 112 : 51;  // offset of a channel's 4 zero words
+  static constexpr int ZCH = ZZERO + 4;            // words per channel
+  static constexpr int ZSLOT = 16 * ZCH;           // words per chunk
+  static_assert(IWE + 4 <= 40 && 40 <= IWP, "B reads reach column 16 + 16 + 7");
+  static_assert((14 + K - 8) / 2 + 4 <= ZWC && 2 * ZWC <= ZROW && K * ZROW <= ZZERO, "Z table");
+};
+
+struct Ed3Lds {  // byte offsets; every block parameter is resident for the whole tile
+  size_t xs, hs, w1, b1, bd, wd, z, pool, total;
+};
+template <int K>
+__host__ __device__ constexpr Ed3Lds ed3_lds(int cin_pad, int hid) {
+  using G = Ed3Geom<K>;  // (the LDS layout does not depend on the workgroup size)
+  const size_t ldx = cin_pad + 8, hp = (size_t)(hid + 15) / 16 * 16;
+  Ed3Lds l{};
+  l.xs = 0;
+  l.hs = (size_t)G::HP * ldx * 2;
+  l.w1 = l.hs + (size_t)2 * 16 * G::CHP * 2;
+  l.b1 = l.w1 + hp * ldx * 2;
+  l.bd = l.b1 + hp * 4;
+  l.wd = l.bd + hp * 4;
+  l.z = l.wd + (hp * K * K * 2 + 15) / 16 * 16;
+  l.pool = l.z + (size_t)2 * G::ZSLOT * 4;
+  l.total = l.pool + hp * 4;
+  return l;
+}
+
+__device__ __forceinline__ unsigned short bf16_bits(float v) {
+  return __builtin_bit_cast(unsigned short, (bf16)v);
+}
+
+// Sum over each 16-lane row by DPP (no LDS round trips): every lane ends with its row's sum.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row_sum_dpp(float v) {
+  v += dpp_f<0xb1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4e>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x124>(v);  // row_ror:4
+  v += dpp_f<0x128>(v);  // row_ror:8
+  return v;
+}
+
+template <int K, int NT_, int OCC>
+__global__ __launch_bounds__(NT_, OCC) void expand_dw3_kernel(EdArgs a) {
+  using G = Ed3Geom<K, NT_>;
+  constexpr int CPW = G::CPW;
+  constexpr int NT = G::NT, IWE = G::IWE, IWP = G::IWP, CHP = G::CHP, KSTEPS = G::KSTEPS, TPW = G::TPW;
+  constexpr int P = (K - 1) / 2;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int ldx = a.cin_pad + 8;
+  const int hp = (a.hid + 15) / 16 * 16;
+  const Ed3Lds L = ed3_lds<K>(a.cin_pad, a.hid);
+  bf16* xs = reinterpret_cast<bf16*>(smem + L.xs);
+  bf16* hs = reinterpret_cast<bf16*>(smem + L.hs);  // [2][16][CHP]
+  bf16* w1s = reinterpret_cast<bf16*>(smem + L.w1);  // [hp][ldx]
+  float* b1s = reinterpret_cast<float*>(smem + L.b1);
+  float* bds = reinterpret_cast<float*>(smem + L.bd);
+  unsigned short* wds = reinterpret_cast<unsigned short*>(smem + L.wd);  // bf16 [hp][K*K]
+  unsigned* zt = reinterpret_cast<unsigned*>(smem + L.z);               // [2][16][ZCH]
+  float* pool_s = reinterpret_cast<float*>(smem + L.pool);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = blockIdx.x % a.n;  // image fastest (SE-pool atomics spread over images)
+  const int b = blockIdx.x / a.n;
+  const int tx = b % a.tiles_x, ty = b / a.tiles_x;
+  const int oy0 = ty * G::TH, ox0 = tx * G::TW;
+  const int iy0 = oy0 - P, ix0 = ox0 - P;
+  const int64_t hw = (int64_t)a.h * a.w;
+  const bf16* x1 = reinterpret_cast<const bf16*>(a.x1);
+  const bf16* x2 = reinterpret_cast<const bf16*>(a.x2);
+  const int nch = hp / 16;
+
+  // ---- prologue: all parameters and the x halo tile into LDS; zero Z and hs columns [IWE, 40) ----
+  {
+    const int vpr = a.cin_pad / 8;  // 16-byte vectors per expand-weight row
+    const uint4* w1g = reinterpret_cast<const uint4*>(a.w1);
+    for (int i = tid; i < hp * vpr; i += NT) {
+      const int r = i / vpr, v = i - r * vpr;
+      *reinterpret_cast<uint4*>(w1s + r * ldx + v * 8) = w1g[i];
+    }
+    for (int i = tid; i < hp; i += NT) {
+      b1s[i] = i < a.hid ? a.b1[i] : 0.f;
+      bds[i] = i < a.hid ? a.bdw[i] : 0.f;
+      pool_s[i] = 0.f;
+    }
+    for (int i = tid; i < hp * K * K; i += NT) wds[i] = i < a.hid * K * K ? bf16_bits(a.wdw[i]) : (unsigned short)0;
+    for (int i = tid; i < 2 * G::ZSLOT; i += NT) zt[i] = 0u;
+    for (int i = tid; i < 2 * 16 * G::IH; i += NT) {
+      unsigned* p = reinterpret_cast<unsigned*>(hs + (i / G::IH) * CHP + (i % G::IH) * IWP + IWE);
+#pragma unroll
+      for (int q = 0; q < (40 - IWE) / 2; ++q) p[q] = 0u;
+    }
+    // x halo tile, channel-minor: xs[p][c]; p = row * IWE + col (cols >= IW duplicate IW-1)
+    const bf16* xb1 = x1 + (int64_t)n * a.c1 * hw;
+    const bf16* xb2 = x2 + (int64_t)n * (a.cin - a.c1) * hw - (int64_t)a.c1 * hw;
+    for (int p = tid; p < G::HP; p += NT) {
+      const int pp = min(p, G::NPE - 1);
+      const int gy = refl(iy0 + pp / IWE, a.hd), gx = refl(ix0 + min(pp % IWE, G::IW - 1), a.wd);
+      const int off = gy * a.w + gx;
+      for (int g0 = 0; g0 < a.cin_pad; g0 += 32) {
+        bf16x8 v[4];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          const int c = g0 + j;
+          bf16 xv = (bf16)0.f;
+          if (c < a.cin) xv = (c < a.c1 ? xb1 : xb2)[(int64_t)c * hw + off];
+          v[j >> 3][j & 7] = xv;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (g0 + 8 * q < a.cin_pad) *reinterpret_cast<bf16x8*>(xs + p * ldx + g0 + 8 * q) = v[q];
+      }
+    }
+  }
+
+  // Toeplitz weights of chunk cc into Z slot cc & 1 (only the weight positions; the rest stays zero)
+  const int zch = tid / (K * K), zky = (tid % (K * K)) / K, zkx = tid % K;
+  unsigned short* zw = reinterpret_cast<unsigned short*>(zt + zch * G::ZCH + zky * G::ZROW) + 7 + zkx;
+  auto build_z = [&](int cc) {
+    if (tid < 16 * K * K) {
+      const unsigned short wb = wds[cc * 16 * K * K + tid];
+      unsigned short* z_ = zw + (cc & 1) * G::ZSLOT * 2;
+      z_[0] = wb;                   // copy 0: element 15 + kx - 8
+      z_[2 * G::ZWC - 1] = wb;      // copy 1: element 15 + kx - 9
+    }
+  };
+
+  // expand: per-lane LDS offsets, fixed over chunks. A wave past the last halo tile recomputes it
+  // and rewrites the same values (no branch); pixel groups past the halo land in the channel pitch's
+  // overhang.
+  const int r16 = lane & 15, q4 = lane >> 4;
+  int xoff[TPW], hoff[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = min(wave + (NT / 64) * i, G::NTILE - 1);
+    xoff[i] = (t * 16 + r16) * ldx;
+    const int p0 = t * 16 + 4 * q4;
+    hoff[i] = r16 * CHP + (p0 / IWE) * IWP + p0 % IWE;
+  }
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  auto expand = [&](int cc, bf16* hbuf) {
+    const bf16* ws = w1s + cc * 16 * ldx + r16 * ldx;
+    const float bias = b1s[cc * 16 + r16];
+    f32x4 acc[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) acc[i] = f32x4{bias, bias, bias, bias};
+    int k0 = 0;
+    for (; k0 + 32 <= a.cin_pad; k0 += 32) {
+      const int kk = k0 + 8 * q4;
+      const bf16x8 fb = *reinterpret_cast<const bf16x8*>(ws + kk);
+      bf16x8 fa[TPW];
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(xs + xoff[i] + kk);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc[i], 0, 0, 0);
+    }
+    if (k0 < a.cin_pad) {  // k = 16 tail
+      const int kk = k0 + 4 * q4;
+      const s4 fb = *reinterpret_cast<const s4*>(ws + kk);
+      s4 fa[TPW];
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) fa[i] = *reinterpret_cast<const s4*>(xs + xoff[i] + kk);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(fa[i], fb, acc[i], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (bf16)hswish(acc[i][j]);
+      *reinterpret_cast<bf16x4*>(hbuf + hoff[i]) = o;
+    }
+  };
+
+  // depthwise: per-lane operand offsets of the MFMA steps (constant over channels and chunks)
+  const int r_ = r16 >> 1, ct_ = r16 & 1;  // this lane's N index (as a B column) -> (row, half)
+  int zoff[KSTEPS], boff[KSTEPS];
+#pragma unroll
+  for (int s = 0; s < KSTEPS; ++s) {
+    const int k0 = 32 * s + 8 * q4, ky = k0 / G::KSEG, x0 = k0 % G::KSEG;
+    const int o = x0 - r16 + 15;  // window start in the zero-padded weight row
+    const int c = o & 1;
+    zoff[s] = (ky < K && o >= 8 && o <= 14 + K) ? ky * G::ZROW + c * G::ZWC + (o - 8 - c) / 2 : G::ZZERO;
+    boff[s] = (r_ + min(ky, K - 1)) * IWP + 16 * ct_ + x0;
+  }
+  const int64_t plane_o = (int64_t)a.ho * a.wo;
+  const int orow = oy0 + r_, ocol = ox0 + 16 * ct_ + 4 * q4;  // this lane's 4 outputs (C[m][n] layout)
+  const bool interior = oy0 + G::TH <= a.ho && ox0 + G::TW <= a.wo && (a.wo % 4) == 0;
+  bf16* dbase = reinterpret_cast<bf16*>(a.d) + (int64_t)n * a.hid * plane_o + (int64_t)orow * a.wo + ocol;
+
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  auto depthwise = [&](int cc, const bf16* hbuf) {
+    // CPW channels per wave; every operand read issued before the MFMA chains
+    u32x4 av[CPW][KSTEPS], bv[CPW][KSTEPS];
+#pragma unroll
+    for (int cw = 0; cw < CPW; ++cw) {
+      const int ch = wave * CPW + cw;
+      const unsigned* zc = zt + (cc & 1) * G::ZSLOT + ch * G::ZCH;
+      const bf16* himg = hbuf + ch * CHP;
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        const unsigned* zp = zc + zoff[s];
+        av[cw][s] = u32x4{zp[0], zp[1], zp[2], zp[3]};
+        const u32x2 b0 = *reinterpret_cast<const u32x2*>(himg + boff[s]);
+        const u32x2 b1 = *reinterpret_cast<const u32x2*>(himg + boff[s] + 4);
+        bv[cw][s] = u32x4{b0[0], b0[1], b1[0], b1[1]};
+      }
+    }
+    f32x4 acc[CPW];
+#pragma unroll
+    for (int cw = 0; cw < CPW; ++cw) {
+      const float bd = bds[cc * 16 + wave * CPW + cw];
+      acc[cw] = f32x4{bd, bd, bd, bd};
+    }
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s)
+#pragma unroll
+      for (int cw = 0; cw < CPW; ++cw)
+        acc[cw] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av[cw][s]),
+                                                          __builtin_bit_cast(bf16x8, bv[cw][s]), acc[cw], 0, 0, 0);
+#pragma unroll
+    for (int cw = 0; cw < CPW; ++cw) {
+      const int hc = cc * 16 + wave * CPW + cw;
+      if (hc >= a.hid) break;  // wave-uniform (the padded tail of the last chunk)
+      float y[4], psum;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] = hswish(acc[cw][j]);
+      bf16* drow = dbase + (int64_t)hc * plane_o;
+      if (interior) {
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (bf16)y[j];
+        psum = (y[0] + y[1]) + (y[2] + y[3]);
+        *reinterpret_cast<bf16x4*>(drow) = o;
+      } else {
+        psum = 0.f;
+        if (orow < a.ho) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (ocol + j < a.wo) {
+              psum += y[j];
+              drow[j] = (bf16)y[j];
+            }
+        }
+      }
+      psum = row_sum_dpp(psum);  // every lane: its 16-lane row's sum; one LDS add per row
+      if (r16 == 0) __hip_atomic_fetch_add(pool_s + hc, psum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  };
+
+  bf16* const hs0 = hs;
+  bf16* const hs1 = hs + 16 * CHP;
+  lds_barrier();  // parameters, xs, zeroed Z and pool
+  build_z(0);
+  expand(0, hs0);
+  lds_barrier();
+  // two chunks per trip so the hidden-image buffers are fixed addresses
+  for (int c = 0; c < nch; c += 2) {
+    if (c + 1 < nch) {
+      build_z(c + 1);
+      expand(c + 1, hs1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    depthwise(c, hs0);
+    lds_barrier();
+    if (c + 1 >= nch) break;
+    if (c + 2 < nch) {
+      build_z(c + 2);
+      expand(c + 2, hs0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    depthwise(c + 1, hs1);
+    lds_barrier();
+  }
+  for (int c = tid; c < a.hid; c += NT) atomicAdd(a.pool + (int64_t)n * a.hid + c, pool_s[c]);
+}
+
+// ------------------------------------------------------------------------------------------------
 // SE MLP + gate folding into the pw-linear weights
 // ------------------------------------------------------------------------------------------------
 template <typename T>
@@ -1176,16 +1498,43 @@ int launch_ed2_auto(EdArgs a, hipStream_t st) {
   return AST_E_UNSUPPORTED;
 }
 
-int g_ed_version = 2;  // AST_MB_ED=1 selects the v1 kernel (A/B measurements)
+int g_ed_version = 3;  // AST_MB_ED=1|2 select the v1|v2 kernels (A/B measurements); 3: v3 where it fits
+
+int g_ed3_nt = 0;  // AST_MB_ED3_NT=512|1024 forces the v3 workgroup size (A/B measurements)
+
+template <int K>
+int launch_ed3(EdArgs a, hipStream_t st) {
+  using G = Ed3Geom<K>;
+  if (a.cin_pad > 256) return AST_E_UNSUPPORTED;
+  const size_t lds = ed3_lds<K>(a.cin_pad, a.hid).total;
+  if (lds > kLdsBudgetMax) return AST_E_UNSUPPORTED;
+  a.tiles_x = (a.wo + G::TW - 1) / G::TW;
+  a.tiles_y = (a.ho + G::TH - 1) / G::TH;
+  const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.n;
+  if (blocks > 0x7fffffffLL) return AST_E_SHAPE;
+  // two 8-wave workgroups per CU when the LDS allows, else one 16-wave workgroup (latency hiding)
+  const bool two = lds <= kLdsBudget;
+  const int nt = g_ed3_nt ? g_ed3_nt : two ? 512 : 1024;
+  auto kern = nt == 512 ? (two ? expand_dw3_kernel<K, 512, 2> : expand_dw3_kernel<K, 512, 1>)
+                        : expand_dw3_kernel<K, 1024, 1>;
+  const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(nt), lds, st, a);
+  return (int)hipGetLastError();
+}
 
 template <typename T>
 int dispatch_ed(EdArgs a, int k, int s, int up, bool expand, hipStream_t st) {
+  if (sizeof(T) == 2 && s == 1 && up == 1 && expand && g_ed_version >= 3) {
+    const int r = k == 3 ? launch_ed3<3>(a, st) : k == 5 ? launch_ed3<5>(a, st) : AST_E_UNSUPPORTED;
+    if (r != AST_E_UNSUPPORTED) return r;
+  }
   if (sizeof(T) == 2 && s == 1 && g_ed_version >= 2) {
     int r = AST_E_UNSUPPORTED;
     if (expand && up == 1 && k == 3) r = launch_ed2_auto<3, 1, true>(a, st);
     // k5 with narrow inputs: v2 only has the 4-row tile here (the 8-row one exceeds 80 KB of LDS),
     // whose halo recompute makes it slower than v1 (measured, scripts/bench_mb_blocks.py)
-    else if (expand && up == 1 && k == 5 && (a.cin_pad > 48 || g_ed_version == 3)) r = launch_ed2_auto<5, 1, true>(a, st);
+    else if (expand && up == 1 && k == 5 && a.cin_pad > 48) r = launch_ed2_auto<5, 1, true>(a, st);
     else if (!expand && k == 3 && up == 1) r = launch_ed2_auto<3, 1, false>(a, st);
     else if (!expand && k == 3 && up == 2) r = launch_ed2_auto<3, 2, false>(a, st);
     if (r != AST_E_UNSUPPORTED) return r;
@@ -1259,7 +1608,7 @@ int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, i
   hipStream_t st = (hipStream_t)stream;
   static const int ver = [] {
     const char* v = getenv("AST_MB_ED");
-    return v ? atoi(v) : 2;
+    return v ? atoi(v) : 3;
   }();
   g_ed_version = ver;
   static const int big = [] {
@@ -1272,9 +1621,14 @@ int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, i
     return v ? atoi(v) : 0;
   }();
   g_ed_th = th;
+  static const int ed3_nt = [] {
+    const char* v = getenv("AST_MB_ED3_NT");
+    return v ? atoi(v) : 0;
+  }();
+  g_ed3_nt = ed3_nt;
   hipError_t e = hipMemsetAsync(pool, 0, sizeof(float) * (size_t)n * hid, st);
   if (e != hipSuccess) return (int)e;
-  EdArgs a{x1, x2, c1, n, cin, h, w, h * up, w * up, ho, wo, w1p, b1, hid, expand ? cin_pad : 0, wdw, bdw, d, pool, 0, 0};
+    EdArgs a{x1, x2, c1, n, cin, h, w, h * up, w * up, ho, wo, w1p, b1, hid, expand ? cin_pad : 0, wdw, bdw, d, pool, 0, 0};
   if (dtype == 0) return dispatch_ed<float>(a, k, stride, up, expand, st);
   if (dtype == 1) return dispatch_ed<bf16>(a, k, stride, up, expand, st);
   return AST_E_UNSUPPORTED;
