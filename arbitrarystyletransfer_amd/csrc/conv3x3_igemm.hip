@@ -774,7 +774,7 @@ __global__ __launch_bounds__(256, 3) void conv3x3_smallc_kernel(ConvArgs a) {
       }
     }
     __syncthreads();
-#pragma unroll 2
+#pragma unroll 1
     for (int c = 0; c < CK; ++c) {  // channels past Cin hold zero inputs and zero weights
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky) {
@@ -783,9 +783,28 @@ __global__ __launch_bounds__(256, 3) void conv3x3_smallc_kernel(ConvArgs a) {
         const float* rowp = As + (c * SR + srow) * RS + C0;
         constexpr int NV = UP == 1 ? 6 : 4;
         float v[NV];
-        const int base = UP == 1 ? 4 * tx - 1 : 2 * tx - 1;
+        if constexpr (UP == 1) {
+          // columns 4tx-1 .. 4tx+4: one aligned 16-byte read (consecutive lanes, conflict-free) and
+          // the two neighbours from the adjacent lanes (DPP wave shifts); the scalar reads at a
+          // 4-word lane stride were 4-way bank conflicts. Each half-wave is one output row, so its
+          // first and last lanes read their outer neighbour themselves.
+          const float4 mid = *reinterpret_cast<const float4*>(rowp + 4 * tx);
+          float left = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, mid.w), 0x138,
+                                                                           0xf, 0xf, false));  // wave_shr:1
+          float right = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, mid.x), 0x130,
+                                                                            0xf, 0xf, false));  // wave_shl:1
+          if (tx == 0) left = rowp[-1];
+          if (tx == 31) right = rowp[128];
+          v[0] = left;
+          v[1] = mid.x;
+          v[2] = mid.y;
+          v[3] = mid.z;
+          v[4] = mid.w;
+          v[5] = right;
+        } else {
 #pragma unroll
-        for (int m = 0; m < NV; ++m) v[m] = rowp[base + m];
+          for (int m = 0; m < NV; ++m) v[m] = rowp[2 * tx - 1 + m];
+        }
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           const float4 w4 = *reinterpret_cast<const float4*>(Ws + (c * 9 + ky * 3 + kx) * 4);  // LDS broadcast
@@ -834,14 +853,16 @@ __global__ __launch_bounds__(256, 3) void conv3x3_smallc_kernel(ConvArgs a) {
 // Normalization of models.py:120-131 applied in the gather). As an implicit GEMM its K = 27 runs
 // in 4-channel K-chunks behind 64-channel MFMA tiles and the launch is bound by writing 21x its
 // input bytes; here a workgroup stages its 8x128-pixel source tile (+halo) once, each thread keeps
-// its 3x6 input window per channel in registers and loops over the output channels 8 at a time:
-// weights are wave-uniform (read once per wave, broadcast), every store is a 512-B row run.
+// its 3x6 input window per channel in registers and loops over the output channels 4 at a time:
+// the workgroup's weights sit in LDS and each tap's 4 output channels are one broadcast 16-byte
+// read (as wave-uniform scalar loads, 108 weights per trip spilled 150 SGPRs: 2 SGPR reloads per
+// FMA pair); every store is a 512-B row run.
 template <int CIN, bool NORM, int TH, bool NTS, int OCC>
 __global__ __launch_bounds__(TH * 32, OCC) void conv3x3_cin4_kernel(ConvArgs a, const float* __restrict__ wp) {
-  // (wp as a noalias kernel argument: the uniform weight reads become scalar loads)
   constexpr int NT = TH * 32, TWS = 128, COG = 4;
   constexpr int SR = TH + 2, RS = TWS + 8, C0 = 4;
   __shared__ __attribute__((aligned(16))) float As[CIN * SR * RS];
+  extern __shared__ __attribute__((aligned(16))) float cin4_w[];  // [CIN * 9][cout_pad]
 
   const int tid = threadIdx.x;
   const int tx = tid & 31, ty = tid >> 5;
@@ -872,6 +893,8 @@ __global__ __launch_bounds__(TH * 32, OCC) void conv3x3_cin4_kernel(ConvArgs a, 
     const bool ok = c < a.Cin && sy >= 0 && sx >= 0;
     sv[i] = ok ? xin[c * plane + max(sy, 0) * W + max(sx, 0)] : 0.f;
   }
+  for (int i = tid; i < CIN * 9 * a.cout_pad / 4; i += NT)
+    reinterpret_cast<float4*>(cin4_w)[i] = reinterpret_cast<const float4*>(wp)[i];
 #pragma unroll
   for (int i = 0; i < ST_T; ++i) {
     const int e = tid + i * NT;
@@ -917,12 +940,12 @@ __global__ __launch_bounds__(TH * 32, OCC) void conv3x3_cin4_kernel(ConvArgs a, 
       for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
         for (int c = 0; c < CIN; ++c) {
-          const float* wr = wp + (c * 9 + ky * 3 + kx) * cout_pad + co0;
+          const float4 w4 = *reinterpret_cast<const float4*>(cin4_w + (c * 9 + ky * 3 + kx) * cout_pad + co0);
+          const float wk[COG] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
           for (int k = 0; k < COG; ++k) {
-            const float w = wr[k];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[k][j] = fmaf(v[c][ky][j + kx], w, acc[k][j]);
+            for (int j = 0; j < 4; ++j) acc[k][j] = fmaf(v[c][ky][j + kx], wk[k], acc[k][j]);
           }
         }
     if (!ok) continue;
@@ -1026,12 +1049,14 @@ int launch_cin4(const ConvArgs& a0, hipStream_t s, int up) {
   if (nblk >= 0x7fffffff) return AST_E_SHAPE;
   const dim3 g((unsigned)nblk), b(TH * 32);
   const bool norm = a.in_mean != nullptr;
+  const size_t wl = (size_t)a.Cin * 9 * a.cout_pad * sizeof(float);  // weights in LDS
+  if (a.cout_pad % 4 || wl > 32 * 1024) return AST_E_UNSUPPORTED;
   if (a.Cin == 3) {
-    if (norm) hipLaunchKernelGGL((conv3x3_cin4_kernel<3, true, TH, NTS, OCC>), g, b, 0, s, a, a.wp);
-    else hipLaunchKernelGGL((conv3x3_cin4_kernel<3, false, TH, NTS, OCC>), g, b, 0, s, a, a.wp);
+    if (norm) hipLaunchKernelGGL((conv3x3_cin4_kernel<3, true, TH, NTS, OCC>), g, b, wl, s, a, a.wp);
+    else hipLaunchKernelGGL((conv3x3_cin4_kernel<3, false, TH, NTS, OCC>), g, b, wl, s, a, a.wp);
   } else {
-    if (norm) hipLaunchKernelGGL((conv3x3_cin4_kernel<4, true, TH, NTS, OCC>), g, b, 0, s, a, a.wp);
-    else hipLaunchKernelGGL((conv3x3_cin4_kernel<4, false, TH, NTS, OCC>), g, b, 0, s, a, a.wp);
+    if (norm) hipLaunchKernelGGL((conv3x3_cin4_kernel<4, true, TH, NTS, OCC>), g, b, wl, s, a, a.wp);
+    else hipLaunchKernelGGL((conv3x3_cin4_kernel<4, false, TH, NTS, OCC>), g, b, wl, s, a, a.wp);
   }
   return (int)hipGetLastError();
 }
