@@ -118,6 +118,8 @@ def train_bench(args, dev, rank, world):
                      "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3),
                      "mfma_tflop_per_step": fl / args.steps / 1e12},
     }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0 and not args.full_losses:
+        result["cpu_baseline"] = cpu_baseline_train(S, args.cpu_seconds, cpu_thread_options(args.cpu_threads))
     if rank == 0:
         print(json.dumps(result), flush=True)
 
@@ -310,6 +312,24 @@ def _cpu_model():
     return f"{cpu_model}, {platform.machine()}"
 
 
+def _usable_cpus():
+    """CPUs this process may run on: the affinity mask and the cgroup v2 quota (None if unknown)."""
+    n = None
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            qn = max(1, int(-(-int(q) // int(per))))
+            n = qn if n is None else min(n, qn)
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_thread_options(requested: int = 0):
     """Thread counts the CPU baseline is timed at: the host's cores (os.cpu_count()),
     the CPUs this process may run on (affinity mask, cgroup quota) and the OMP_NUM_THREADS the box
@@ -337,24 +357,49 @@ def cpu_thread_options(requested: int = 0):
 
 
 def time_cpu(run_one, seconds, thread_opts, max_items=64):
-    """Time `run_one()` (one unit of CPU work) at each thread count for seconds/len(opts) each
-    (at least one unit); returns (best rate, its threads, {threads: rate}, units, elapsed)."""
-    rates, best = {}, None
-    budget = seconds / len(thread_opts)
+    """Time `run_one()` (one unit of CPU work) at the candidate thread counts; returns (best rate,
+    its threads, {threads: rate}, units, elapsed, note). Every candidate first runs the small
+    warm-up unit; a count whose warm-up is over 2x the fastest one (oversubscribed: the host's
+    os.cpu_count() can far exceed the CPUs this process may use) is not timed further -- one
+    full-size unit there can take minutes; a count above the CPUs this process may run on is not
+    even warmed up. The rest share `seconds` (at least one unit each).
+    Progress goes to stderr so a long baseline is visibly alive."""
+    # thread counts beyond the CPUs this process may run on (affinity mask, cgroup quota) only
+    # oversubscribe them: on the GPU box os.cpu_count() is the whole host (256) against a 16-CPU
+    # share, where one warm-up unit at 256 threads took minutes
+    allowed = _usable_cpus()
+    warm = {}
     for th in thread_opts:
+        if allowed and th > allowed:
+            continue
         torch.set_num_threads(th)
         run_one(warmup=True)
+        t0 = time.perf_counter()
+        run_one(warmup=True)
+        warm[th] = time.perf_counter() - t0
+        print(f"[cpu baseline] warm-up at {th} threads: {warm[th]:.3f} s", file=sys.stderr, flush=True)
+    fastest = min(warm.values())
+    timed = [th for th in thread_opts if th in warm and warm[th] <= 2.0 * fastest]
+    skipped = {th: (warm[th] / fastest if th in warm else None) for th in thread_opts if th not in timed}
+    rates, best = {}, None
+    budget = seconds / len(timed)
+    for th in timed:
+        torch.set_num_threads(th)
         n, t0 = 0, time.perf_counter()
         while True:
             run_one(warmup=False)
             n += 1
             dt = time.perf_counter() - t0
+            print(f"[cpu baseline] {th} threads: {n} unit(s) in {dt:.1f} s", file=sys.stderr, flush=True)
             if dt >= budget or n >= max_items:
                 break
         rates[th] = n / dt
         if best is None or rates[th] > best[0]:
             best = (rates[th], th, n, dt)
-    return best[0], best[1], rates, best[2], best[3]
+    note = "".join(f"; {th} threads not timed (warm-up {r:.1f}x the fastest)" if r is not None else
+                   f"; {th} threads not timed (more than the {allowed} CPUs this process may use)"
+                   for th, r in skipped.items())
+    return best[0], best[1], rates, best[2], best[3], note
 
 
 def cpu_baseline_mobilenet(size, seconds, thread_opts, attention=False):
@@ -376,11 +421,35 @@ def cpu_baseline_mobilenet(size, seconds, thread_opts, attention=False):
             else:
                 R.mb_style_transfer(c, s, *sds, **kw)
 
-    rate, th, rates, n, dt = time_cpu(one, seconds, thread_opts)
+    rate, th, rates, n, dt, note = time_cpu(one, seconds, thread_opts)
     return {"value": rate, "unit": "images/s", "cores": th, "kind": "port",
             "sample": f"{n} content+style pair(s) of 1x3x{size}x{size}, MobileNet variant, fp32 torch CPU "
                       f"({_cpu_model()}, os.cpu_count()={os.cpu_count()}), {dt:.1f} s; images/s by threads: "
-                      + ", ".join(f"{k}: {v:.3f}" for k, v in rates.items())}
+                      + ", ".join(f"{k}: {v:.3f}" for k, v in rates.items()) + note}
+
+
+def cpu_baseline_train(size, seconds, thread_opts):
+    """The CPU oracle's AdaIN training step (oracle.ref_cpu.train_step: the same losses, backward,
+    clip 2.0 + Adam on the decoder) on single image pairs."""
+    from oracle import ref_cpu as R
+    enc = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_encoder_weights(1)]
+    dec0 = [(torch.from_numpy(w), torch.from_numpy(b)) for w, b in synth.vgg_decoder_weights(2)]
+    c = torch.from_numpy(synth.image(779, (1, 3, size, size)))
+    s = torch.from_numpy(synth.image(780, (1, 3, size, size)))
+
+    def one(warmup):
+        dec = [(w.clone(), b.clone()) for w, b in dec0]
+        if warmup:
+            R.train_step(c[:, :, :64, :64], s[:, :, :64, :64], enc, dec)
+        else:
+            R.train_step(c, s, enc, dec)
+
+    rate, th, rates, n, dt, note = time_cpu(one, seconds, thread_opts)
+    return {"value": rate, "unit": "images/s", "cores": th, "kind": "port",
+            "sample": f"{n} training step(s) on one 1x3x{size}x{size} content+style pair (AdaIN decoder, VGG loss "
+                      f"network, content+style+lf+tv, clip + Adam), fp32 torch CPU ({_cpu_model()}, "
+                      f"os.cpu_count()={os.cpu_count()}), {dt:.1f} s; images/s by threads: "
+                      + ", ".join(f"{k}: {v:.3f}" for k, v in rates.items()) + note}
 
 
 def cpu_baseline(size, seconds, thread_opts):
@@ -398,11 +467,11 @@ def cpu_baseline(size, seconds, thread_opts):
             else:
                 R.style_transfer(c, s, enc, dec)
 
-    rate, th, rates, n, dt = time_cpu(one, seconds, thread_opts)
+    rate, th, rates, n, dt, note = time_cpu(one, seconds, thread_opts)
     return {"value": rate, "unit": "images/s", "cores": th, "kind": "port",
             "sample": f"{n} content+style pair(s) of 1x3x{size}x{size}, VGG relu4_1 -> AdaIN -> decoder, "
                       f"fp32 torch CPU ({_cpu_model()}, os.cpu_count()={os.cpu_count()}), {dt:.1f} s; "
-                      "images/s by threads: " + ", ".join(f"{k}: {v:.3f}" for k, v in rates.items())}
+                      "images/s by threads: " + ", ".join(f"{k}: {v:.3f}" for k, v in rates.items()) + note}
 
 
 def launch_ranks(args) -> int:
