@@ -51,9 +51,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="0 = best of os.cpu_count(), the affinity/cgroup CPU share and OMP_NUM_THREADS")
-    p.add_argument("--mode", choices=["fwd", "train", "mobilenet", "ae-train"], default="fwd",
+    p.add_argument("--mode", choices=["fwd", "train", "mobilenet", "ae-train", "ast-train"], default="fwd",
                    help="fwd: config 2 (the headline metric); train: config 3/4 AdaIN training step; "
-                        "mobilenet: config 5; ae-train: train_autoencoder.py step (SURVEY §8f next #4)")
+                        "mobilenet: config 5; ae-train: train_autoencoder.py step (SURVEY §8f next #4); "
+                        "ast-train: train.py's ASTTrainer step (MobileNet AST + AdaAttN)")
     p.add_argument("--full-losses", action="store_true",
                    help="train mode: add train.py's hist, org_img and out_of_range terms (SURVEY §8f next #2)")
     p.add_argument("--attention", action="store_true",
@@ -173,8 +174,71 @@ def ae_train_bench(args, dev, rank, world):
                                f"perceptual Huber via VGG relu_1..relu_15; clip 10 + Adam), bs={B}/GPU {S}x{S} fp32",
                    "global_batch": B * world, "image_size": S,
                    "parallelism": f"data-parallel x{world}" + (" + SyncBatchNorm" if world > 1 else "")},
-        "roofline": {"bound": "mfma", "kernel": "conv3x3 fwd/dgrad + wgrad MFMA launches of a step",
-                     "achieved": tf, "peak": PEAK_FP32_MFMA_TF, "unit": "TFLOP/s", "frac": tf / PEAK_FP32_MFMA_TF,
+        "roofline": {"bound": "mfma", "kernel": "loss-network conv3x3 fwd/dgrad launches of a step (split-bf16)",
+                     "achieved": tf, "peak": PEAK_SPLIT_BF16_TF, "unit": "TFLOP/s", "frac": tf / PEAK_SPLIT_BF16_TF,
+                     "fp32_mfma_peak": PEAK_FP32_MFMA_TF, "frac_of_fp32_mfma_peak": tf / PEAK_FP32_MFMA_TF,
+                     "traffic": None, "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3)},
+        "kernels_ms_per_step": {k: round(m / args.steps, 4) for k, (f, m, c) in sorted(fam.items())},
+        "mbgemm_tflops": (fam["mbgemm"][0] / (fam["mbgemm"][1] * 1e-3) / 1e12) if "mbgemm" in fam else None,
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def ast_train_bench(args, dev, rank, world):
+    """The reference's own trainer step, ASTTrainer (train.py:186-300; SURVEY §8f next #1 with
+    its caller): the MobileNet AST with AdaAttN in training mode, the four VGG loss-network
+    passes, every train.py loss term, backward through decoder / ada_out / AdaAttN / encoder,
+    clip 2.0 + Adam over ast.parameters(). bs=8 (train.py:408) at 160x160 (the largest of
+    conf.py img_sizes). N > 1: data parallel, bs=8 per rank, SyncBatchNorm + one gradient
+    all-reduce."""
+    from arbitrarystyletransfer_amd.train import ASTTrainer, default_ast_args
+    B, S = args.batch or 8, args.size or 160
+    trainer = ASTTrainer(default_ast_args(batch_size=B * world), device=dev,
+                         ast=models.AST(attention=True).load_live_init())
+    content = torch.from_numpy(synth.image(905 + rank, (B, 3, S, S))).to(dev)
+    style = torch.from_numpy(synth.image(925 + rank, (B, 3, S, S))).to(dev)
+    for _ in range(args.warmup):
+        trainer.train_step(content, style, record=False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    timer = ops.LaunchTimer()
+    t0 = time.perf_counter()
+    with timer:
+        for _ in range(args.steps):
+            out = trainer.train_step(content, style, record=False)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out["loss"]), "non-finite loss"
+    fam = {}
+    for tag, fl, ms in timer.results():
+        k = tag.split()[0]
+        f0, m0, c0 = fam.get(k, (0.0, 0.0, 0))
+        fam[k] = (f0 + fl, m0 + ms, c0 + 1)
+    mm = [fam[k] for k in fam if k.startswith(("conv3x3", "wgrad"))]
+    fl, ms = sum(f for f, _, _ in mm), sum(m for _, m, _ in mm)
+    tf = fl / (ms * 1e-3) / 1e12 if ms else 0.0
+    result = {
+        "metric": "AST training images/sec (train.py ASTTrainer step, MobileNet AST + AdaAttN)",
+        "value": B * world * args.steps / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (live-init weights, U[0,1) images), resident in HBM",
+        "config": {"workload": f"ASTTrainer step (MobileNet AST + AdaAttN in train mode; content, style, lf, tv, hist, "
+                               f"org_img, out_of_range losses via the VGG loss network; clip 2.0 + Adam), "
+                               f"bs={B}/GPU {S}x{S} fp32",
+                   "global_batch": B * world, "image_size": S,
+                   "parallelism": f"data-parallel x{world}" + (" + SyncBatchNorm" if world > 1 else "")},
+        "roofline": {"bound": "mfma", "kernel": "loss-network conv3x3 fwd/dgrad launches of a step (split-bf16)",
+                     "achieved": tf, "peak": PEAK_SPLIT_BF16_TF, "unit": "TFLOP/s", "frac": tf / PEAK_SPLIT_BF16_TF,
+                     "fp32_mfma_peak": PEAK_FP32_MFMA_TF, "frac_of_fp32_mfma_peak": tf / PEAK_FP32_MFMA_TF,
                      "traffic": None, "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3)},
         "kernels_ms_per_step": {k: round(m / args.steps, 4) for k, (f, m, c) in sorted(fam.items())},
         "mbgemm_tflops": (fam["mbgemm"][0] / (fam["mbgemm"][1] * 1e-3) / 1e12) if "mbgemm" in fam else None,
@@ -532,8 +596,9 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    if args.mode in ("train", "mobilenet", "ae-train"):
-        {"train": train_bench, "mobilenet": mobilenet_bench, "ae-train": ae_train_bench}[args.mode](args, dev, rank, world)
+    if args.mode in ("train", "mobilenet", "ae-train", "ast-train"):
+        {"train": train_bench, "mobilenet": mobilenet_bench, "ae-train": ae_train_bench,
+         "ast-train": ast_train_bench}[args.mode](args, dev, rank, world)
         if world > 1:
             dist.destroy_process_group()
         return

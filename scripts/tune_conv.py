@@ -60,6 +60,32 @@ def ae_shapes(batch=16, size=160):
     return seen
 
 
+def adain_train_shapes(batch=16, size=512):
+    """The conv3x3 launches of one AdaIN training step (bench.py --mode train, config 3: decoder,
+    loss network, their input-gradient convs), captured from a live step."""
+    from arbitrarystyletransfer_amd.train import AdaINTrainer, default_args
+    seen = []
+    orig = ops.conv3x3
+
+    def spy(x, w_packed, bias, cout, *, upsample=1, pad_mode="zeros", want_pool=False, x2=None, **kw):
+        n = int(x.shape[0]) + (int(x2.shape[0]) if x2 is not None else 0)
+        shp = (n, int(x.shape[1]), int(x.shape[2]), int(x.shape[3]), cout, upsample, pad_mode, want_pool)
+        if shp not in seen:
+            seen.append(shp)
+        return orig(x, w_packed, bias, cout, upsample=upsample, pad_mode=pad_mode, want_pool=want_pool, x2=x2, **kw)
+
+    ops.conv3x3 = spy
+    try:
+        tr = AdaINTrainer(default_args(batch_size=batch), device="cuda")
+        c = torch.from_numpy(synth.image(903, (batch, 3, size, size))).cuda()
+        s = torch.from_numpy(synth.image(904, (batch, 3, size, size))).cuda()
+        tr.train_step(c, s, record=False)
+        torch.cuda.synchronize()
+    finally:
+        ops.conv3x3 = orig
+    return seen
+
+
 def key(n, cin, h, w, cout, up, pad, pool):
     return f"{n}x{cin}x{h}x{w}->{cout} up{up} {pad}{' pool' if pool else ''}"
 
@@ -94,7 +120,10 @@ def main():
     if os.path.exists(path):
         table = json.load(open(path))
     report = []
-    todo = ae_shapes() if os.environ.get("TUNE_AE") else shapes(batch)
+    todo = ae_shapes() if os.environ.get("TUNE_AE") else adain_train_shapes() if os.environ.get("TUNE_TRAIN") \
+        else shapes(batch)
+    if os.environ.get("TUNE_NEW"):  # only shapes the table does not hold yet
+        todo = [t for t in todo if key(*t) not in table]
     if os.environ.get("TUNE_SMALL"):  # only the shapes the direct VALU kernels serve (cin or cout <= 4)
         todo = [t for t in todo if t[1] <= 4 or t[4] <= 4]
     for shp in todo:
