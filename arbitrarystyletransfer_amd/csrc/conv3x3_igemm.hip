@@ -464,6 +464,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 struct defeats SROA: scratch)
 
 constexpr int kX3K = 16;  // input channels per chunk (= the MFMA K)
+#ifndef X3_STAGED_EPI
+#define X3_STAGED_EPI 1  // epilogue through LDS (store_tiles_staged); 0 = direct stores (A/B)
+#endif
 
 __host__ __device__ constexpr int64_t x3_split_offset(int cin, int cout) {  // floats before the split part
   return (int64_t)((cin + 7) / 8 * 8) * 9 * ((cout + 63) / 64 * 64);
@@ -511,12 +514,93 @@ struct X3Cfg {
   static constexpr int A_T = (A_PLANE + NT - 1) / NT;  // gather items per thread (one item = 8 channels)
   static constexpr int B_T = (B_UNITS + NT - 1) / NT;
   static constexpr int NS = UP == 1 ? RM + 2 : RM / 2 + 2;  // source rows a wave's RM output rows read
-  static constexpr int LDS_BYTES = (A_UNITS + B_UNITS) * 16;
+  static constexpr int LDS_TILES = (A_UNITS + B_UNITS) * 16;
+  static constexpr int LDS_EPI = X3_STAGED_EPI ? WM * 32 * RM * 36 * 4 : 0;  // staged epilogue regions
+  static constexpr int LDS_BYTES = LDS_TILES > LDS_EPI ? LDS_TILES : LDS_EPI;
 };
 
 // source row (relative to the wave's first) of output row i at tap row ky
 template <int UP>
 __host__ __device__ constexpr int x3_srel(int i, int ky) { return UP == 1 ? i + ky : ((i + ky - 1) >> 1) + 1; }
+
+// Epilogue through LDS (x3 kernel): in the MFMA layout a lane holds one output channel, so a
+// direct float4 store scatters over 64 rows/planes per instruction (store-issue-bound). Each wave
+// writes its accumulators (+bias) to its own LDS region [32 channels][RM rows][32 px + 4], then
+// stores rows: 8 lanes per 128-byte run, pre-ReLU / ReLU / 2x2 max-pool as store_tiles. The
+// caller's barrier must precede it (the region overlaps the operand tiles).
+template <int RM, int RN>
+__device__ __forceinline__ void store_tiles_staged(const ConvArgs& a, const f32x16 (&acc)[RM][RN], int n, int x0,
+                                                   int y0, int row0, int n0c, int h, int l32, int lane,
+                                                   float* __restrict__ region) {
+  constexpr int RP = 36;  // row pitch (floats): 32 px + 4
+  const int H = a.H, W = a.W;
+  const int64_t plane = (int64_t)H * W;
+  const bool vec4 = (W & 3) == 0;
+  const int Ho = H >> 1, Wo = W >> 1;
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    {
+      const int co = n0c + j * 32 + l32;
+      const float bv = (co < a.Cout && a.bias) ? a.bias[co] : 0.f;
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(region + (l32 * RM + i) * RP + 8 * g + 4 * h) =
+              make_float4(acc[i][j][4 * g] + bv, acc[i][j][4 * g + 1] + bv, acc[i][j][4 * g + 2] + bv,
+                          acc[i][j][4 * g + 3] + bv);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done
+    __builtin_amdgcn_wave_barrier();
+    if (a.y_pre || a.y_act) {
+#pragma unroll
+      for (int it = 0; it < 32 * RM * 8 / 64; ++it) {
+        const int item = it * 64 + lane;
+        const int q = item & 7, row = (item >> 3) % RM, ch = item / (8 * RM);
+        const int co = n0c + j * 32 + ch, yy = y0 + row0 + row, xx = x0 + 4 * q;
+        if (co >= a.Cout || yy >= H || xx >= W) continue;
+        const float4 v = *reinterpret_cast<const float4*>(region + (ch * RM + row) * RP + 4 * q);
+        const int64_t off = ((int64_t)n * a.Cout + co) * plane + (int64_t)yy * W + xx;
+        const bool full = vec4 && xx + 3 < W;
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        if (a.y_pre) {
+          if (full) *reinterpret_cast<float4*>(a.y_pre + off) = v;
+          else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_pre[off + r] = vv[r];
+        }
+        if (a.y_act) {
+          const float4 u = make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
+          if (full) *reinterpret_cast<float4*>(a.y_act + off) = u;
+          else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_act[off + r] = relu_f(vv[r]);
+        }
+      }
+    }
+    if (a.y_pool) {
+#pragma unroll
+      for (int it = 0; it < 32 * (RM / 2) * 8 / 64; ++it) {
+        const int item = it * 64 + lane;
+        const int q = item & 7, prow = (item >> 3) % (RM / 2), ch = item / (8 * (RM / 2));
+        const int co = n0c + j * 32 + ch, py = (y0 + row0) / 2 + prow, px = (x0 + 4 * q) >> 1;
+        if (co >= a.Cout || py >= Ho || px >= Wo) continue;
+        const float4 r0 = *reinterpret_cast<const float4*>(region + (ch * RM + 2 * prow) * RP + 4 * q);
+        const float4 r1 = *reinterpret_cast<const float4*>(region + (ch * RM + 2 * prow + 1) * RP + 4 * q);
+        const float m0 = max_nan(relu_f(r0.x), relu_f(r1.x)), m1 = max_nan(relu_f(r0.y), relu_f(r1.y));
+        const float m2 = max_nan(relu_f(r0.z), relu_f(r1.z)), m3 = max_nan(relu_f(r0.w), relu_f(r1.w));
+        const float p0 = max_nan(m0, m1), p1 = max_nan(m2, m3);
+        const int64_t off = ((int64_t)n * a.Cout + co) * Ho * Wo + (int64_t)py * Wo + px;
+        if (px + 1 < Wo && (Wo & 1) == 0) {
+          *reinterpret_cast<float2*>(a.y_pool + off) = make_float2(p0, p1);
+        } else {
+          a.y_pool[off] = p0;
+          if (px + 1 < Wo) a.y_pool[off + 1] = p1;
+        }
+      }
+    }
+    if (j + 1 < RN) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();  // reads of this j done before the next j's writes
+    }
+  }
+}
 
 template <int WM, int RM, int RN, int UP, int OCC>
 __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
@@ -680,7 +764,13 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   }
 #undef X3_LOAD
 #undef X3_STORE
+#if X3_STAGED_EPI
+  __syncthreads();  // every wave is done reading the last chunk's tiles
+  store_tiles_staged<RM, RN>(a, acc, n, x0, y0, wm * RM, n0, h, l32, lane,
+                             reinterpret_cast<float*>(x3_smem) + wm * 32 * RM * 36);
+#else
   store_tiles<RM, RN>(a, acc, n, x0, y0, wm * RM, n0, h, l32);
+#endif
 }
 
 // Direct (VALU) 3x3 conv for cout <= 4 — the decoder's final 64->3 conv (models.py:627). As a
