@@ -53,6 +53,8 @@ BLOCKS = [
     (24, 24, 1, 1, 3, False, True, (2, 12, 20), 1),    # ratio-1, no upsample
     (96, 80, 1, 4, 5, False, True, (1, 16, 16), 1),
     (16, 16, 1, 6, 3, False, True, (1, 3, 5), 1),      # tiny map (reflect pad on 3 rows)
+    (20, 20, 1, 6, 3, False, True, (2, 12, 40), 1),    # hidden 120: a partial last 16-channel chunk
+    (36, 36, 1, 3, 5, True, True, (1, 19, 70), 1),     # hidden 108, k5, ragged tiles both ways
 ]
 
 
