@@ -1,0 +1,31 @@
+// Shared between mobilenet.hip (v1-v3 expand+depthwise kernels, SE, pw, launch dispatch) and
+// mb_ed4.hip (the v4 expand+depthwise kernel, compiled separately without SLP vectorisation).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace ast_mb {
+
+// Arguments of one expand (+BN, Hardswish) -> depthwise kxk (+BN, Hardswish) -> SE-pool launch
+// (DepthWiseConv, mobilenetv2.py:95-165, up to the SE gate).
+struct EdArgs {
+  const void* x1;
+  const void* x2;   // channels [c1, cin) come from x2 (torch.cat fused away), may equal x1
+  int c1;
+  int n, cin, h, w;  // x geometry (pre-upsample)
+  int hd, wd;        // depthwise input grid (= h*up, w*up)
+  int ho, wo;        // depthwise output
+  const void* w1;    // expand weights T [hid_pad16][cin_pad] (BN folded); null -> ratio-1 block
+  const float* b1;   // [hid]
+  int hid, cin_pad;
+  const float* wdw;  // depthwise weights [hid][k*k] (BN folded)
+  const float* bdw;  // [hid]
+  void* d;           // [n][hid][ho][wo]
+  float* pool;       // [n][hid], accumulated
+  int tiles_x, tiles_y;
+};
+
+// v4 (bf16, stride 1, no upsample, expand blocks with c1 == cin, cin_pad in {16..96, 128}, k in {3, 5}):
+// returns AST_E_UNSUPPORTED when the shape is outside that set (the caller falls back to v3).
+int launch_ed4(EdArgs a, int k, hipStream_t st);
+
+}  // namespace ast_mb

@@ -1,0 +1,283 @@
+// MobileNet expand + depthwise, v4: see the comment below.
+// Its own translation unit because it is built with -fno-slp-vectorize (Makefile): the depthwise taps
+// are scalar v_fma_f32 by design -- on gfx950 v_pk_fma_f32 issues at half rate, so SLP packing the
+// independent taps bought no throughput and cost ~120 register shuffles per input row.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/ast_hip.h"
+#include "mb_common.h"
+
+namespace ast_mb {
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Reflection-pad source index for i in [-(n-1), 2n-2]; clamped for out-of-tile garbage lanes.
+__device__ __forceinline__ int refl(int i, int n) {
+  i = i < 0 ? -i : i;
+  i = i >= n ? 2 * n - 2 - i : i;
+  return min(max(i, 0), n - 1);
+}
+
+__device__ __forceinline__ unsigned short bf16_bits(float v) {
+  return __builtin_bit_cast(unsigned short, (bf16)v);
+}
+
+// ------------------------------------------------------------------------------------------------
+// expand + depthwise, v4 (bf16, stride 1, expand blocks): the hidden rows never leave registers
+// ------------------------------------------------------------------------------------------------
+// v3 reads ~32 B of LDS per depthwise output (Toeplitz operands) and is LDS/latency-bound. Here one
+// wave owns 32 hidden channels of a strip of 32 input columns and slides down a band of rows:
+//   expand:    C[pixel][channel] = X[pixel][cin] . W1^T on v_mfma_f32_32x32x16_bf16. In its C layout
+//              (col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)) a lane holds ONE
+//              channel and 16 pixels; the A rows are assigned so that these are 16 consecutive
+//              columns in register order (lane half 0: columns 0..15, half 1: 16..31).
+//   depthwise: per input row Hardswish in registers; the two columns across the half boundary come
+//              from the partner lane (l ^ 32). Each input row is added into the K output rows it
+//              touches (K rotating register accumulators: static indices by unrolling the row loop
+//              by K); an output row is finished after its last input row (+bias, Hardswish, SE pool
+//              sum, bf16).
+//   store:     per output row the wave's 32 channels x 28 columns pass through a small LDS image so
+//              the D writes are 8-byte pieces, 7 consecutive lanes per channel row.
+// A strip of 32 input columns yields 28 outputs (x0 = 28 s - 2, outputs at local columns 2..29 for
+// both kernel sizes, which keeps the D pieces 8-byte aligned); a band of TH output rows reads
+// TH + K - 1 input rows. x is read straight from global memory (8 channels of one pixel per lane and
+// k-step; the other channel blocks of the strip read the same bytes from L2). The hidden activation
+// stays fp32 (v3 rounds it to bf16 in LDS). One wave per workgroup: no barrier but the wave's own.
+__device__ __forceinline__ float hswish_fast(float v) {  // x * clamp(x/6 + 1/2, 0, 1): within 2 ulp of hswish
+  return v * __builtin_amdgcn_fmed3f(fmaf(v, 1.f / 6.f, 0.5f), 0.f, 1.f);
+}
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+#ifndef ED4_PD
+#define ED4_PD 0  // x rows in flight beyond the next one
+#endif
+#ifndef ED4_TH
+#define ED4_TH 31  // output rows per band (TH + K - 1 a multiple of K for K = 3, 5)
+#endif
+
+template <int K, int KS, int TH, int PD, bool VEC>
+__global__ __launch_bounds__(64, (K == 5 && KS >= 6) ? 1 : 2) void expand_dw4_kernel(EdArgs a, int strips, int bands, int ncb, int total) {
+  constexpr int P = (K - 1) / 2, NJ = TH + K - 1, OW = 28, SP = 40;  // SP: staging row pitch (bf16)
+  __shared__ __align__(16) bf16 stage[32 * SP];
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  // XCD-aware order (workgroup b runs on XCD b % 8): consecutive logical ids -- the channel blocks
+  // of one strip, which read the same x -- share an XCD and its L2
+  const int per = (total + 7) >> 3;
+  const int L = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (L >= total) return;
+  const int cb = L % ncb;
+  int rest = L / ncb;
+  const int s = rest % strips;
+  rest /= strips;
+  const int band = rest % bands;
+  const int n = rest / bands;
+  const int x0 = s * OW - 2, y0 = band * TH;
+  const int ch = cb * 32 + r;
+  const bool chv = ch < a.hid;
+
+  float wk[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) wk[i] = chv ? a.wdw[ch * K * K + i] : 0.f;
+  const float bd = chv ? a.bdw[ch] : 0.f, b1 = chv ? a.b1[ch] : 0.f;
+  const int hid16 = (a.hid + 15) / 16 * 16;
+  bf16x8 bw[KS];  // B[k = 8h + j][col r] = W1[ch][16 s + 8h + j]
+#pragma unroll
+  for (int q = 0; q < KS; ++q)
+    bw[q] = ch < hid16 ? *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.w1) +
+                                                          (int64_t)ch * a.cin_pad + 16 * q + 8 * h)
+                       : bf16x8{};
+
+  // A[row r][k = 8h + j] = x[channel 16 s + 8h + j][pixel pc(r)]
+  const int pc = 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3);
+  const int gx = refl(x0 + pc, a.wd);
+  const int hw2 = 2 * a.h * a.w;  // bytes per channel plane (host-checked: cin * hw2 < 2^31)
+  // one buffer descriptor per image: channels >= cin (the zero-weight padding of the last k-step)
+  // fall outside its range and load as 0; x2 is not used (the host takes v4 only for c1 == cin)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(reinterpret_cast<const bf16*>(a.x1) + (int64_t)n * a.cin * (hw2 / 2)), 0, a.cin * hw2,
+      0x00020000);
+  // raw 16-bit x values of the rows in flight, packed into MFMA fragments only when their row starts:
+  // packing right after the loads (what the compiler does with a bf16x8 built from the loads) makes
+  // the wave wait for them at once, so no load would overlap the VALU work
+  unsigned xraw[PD + 1][KS][8];
+  auto load_row = [&](int j, unsigned (*raw)[8]) {
+    const int vrow = 8 * h * hw2 + 2 * (refl(y0 - P + j, a.hd) * a.w + gx);
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) raw[q][e] = __builtin_amdgcn_raw_buffer_load_b16(xr, vrow + (16 * q + e) * hw2, 0, 0);
+  };
+
+  const int64_t plane_o = (int64_t)a.ho * a.wo;
+  // D through a per-image buffer descriptor: a piece that must not be written (past the right or
+  // bottom border, a padding channel, the unused lanes of the last pass) gets an offset outside the
+  // range and is dropped by the hardware, so every row issues the same stores on every path -- with
+  // a data-dependent store count the compiler's vmcnt bookkeeping degrades to waiting for all stores
+  // before the next row's x fragments can be used
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<bf16*>(a.d) + (int64_t)n * a.hid * plane_o, 0, (int)(2 * a.hid * plane_o), 0x00020000);
+  constexpr unsigned kDrop = 0x80000000u;
+  const bool edge = x0 + 2 + OW > a.wo;  // last strip: outputs past the right border
+  float psum = 0.f;
+  auto finish = [&](int orow, const float* v, bool live) {
+    const int oy = y0 + orow;
+    const bool rowv = live && oy < a.ho;  // uniform
+    float y[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) y[i] = hswish_fast(v[i]);
+    // SE pool: valid local columns are 2..15 (half 0) and 16..29 (half 1)
+    float t = 0.f;
+    if (!edge) {
+      t = h ? y[0] + y[1] : y[14] + y[15];
+#pragma unroll
+      for (int i = 2; i < 14; ++i) t += y[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int lc = 16 * h + i;
+        t += (lc >= 2 && lc < 30 && x0 + lc < a.wo) ? y[i] : 0.f;
+      }
+    }
+    psum += rowv ? t : 0.f;
+    unsigned pk[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      pk[i] = (unsigned)bf16_bits(y[2 * i]) | ((unsigned)bf16_bits(y[2 * i + 1]) << 16);
+    uint4* sw = reinterpret_cast<uint4*>(stage + r * SP + 16 * h);
+    sw[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    sw[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+    lds_barrier();
+#pragma unroll
+    for (int t4 = 0; t4 < 4; ++t4) {
+      const int q = lane + 64 * t4;  // 32 channel rows x 7 pieces of local columns 2+4i .. 5+4i
+      const int cl = min(q / 7, 31), i4 = q - 7 * (q / 7);
+      const unsigned* sp = reinterpret_cast<const unsigned*>(stage + cl * SP + 2 + 4 * i4);
+      const unsigned v0 = sp[0], v1 = sp[1];
+      const int xg = x0 + 2 + 4 * i4;
+      const bool ok = rowv && q < 224 && cb * 32 + cl < a.hid;
+      const unsigned base = (unsigned)(2 * ((cb * 32 + cl) * plane_o + (int64_t)oy * a.wo + xg));
+      if constexpr (VEC) {
+        const unsigned off = ok && xg + 4 <= a.wo ? base : kDrop;
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{v0, v1}, dr, (int)off, 0, 0);
+      } else {
+        const unsigned short e4[4] = {(unsigned short)v0, (unsigned short)(v0 >> 16), (unsigned short)v1,
+                                      (unsigned short)(v1 >> 16)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          __builtin_amdgcn_raw_buffer_store_b16(e4[e], dr, (int)(ok && xg + e < a.wo ? base + 2 * e : kDrop), 0, 0);
+      }
+    }
+    // the next row's staging writes follow these reads in this wave's program order
+  };
+
+  // Every row issues the same loads and stores on every path (NJ % K == 0, the next row is loaded
+  // even past the band -- refl keeps it in bounds -- and finish runs for every row, its stores dropped
+  // when the row is not an output row): the compiler then waits at each row start only for the x
+  // loads, not for the D stores issued after them.
+  static_assert(NJ % K == 0, "TH + K - 1 must be a multiple of K");
+  float acc[K][16];
+#pragma unroll
+  for (int d = 0; d <= PD; ++d) load_row(d, xraw[d]);
+  for (int jb = 0; jb < NJ; jb += K) {
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+      const int j = jb + u;
+      f32x16 c;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) c[i] = b1;
+#pragma unroll
+      for (int q = 0; q < KS; ++q) {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f[e] = (xraw[0][q][2 * e] & 0xffffu) | (xraw[0][q][2 * e + 1] << 16);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f), bw[q], c, 0, 0, 0);
+      }
+#pragma unroll
+      for (int d = 0; d < PD; ++d)
+#pragma unroll
+        for (int q = 0; q < KS; ++q)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xraw[d][q][e] = xraw[d + 1][q][e];
+      load_row(j + PD + 1, xraw[PD]);  // in flight during this row's VALU work
+      float e[20];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) e[2 + i] = hswish_fast(c[i]);
+      const float r0 = __shfl_xor(h ? e[2] : e[16], 32, 64), r1 = __shfl_xor(h ? e[3] : e[17], 32, 64);
+      e[0] = r0;   // half 1: columns 14, 15 (half 0's are never used: its outputs 0, 1 are halo)
+      e[1] = r1;
+      e[18] = r0;  // half 0: columns 16, 17 (likewise unused by half 1)
+      e[19] = r1;
+#pragma unroll
+      for (int ky = K - 1; ky >= 0; --ky) {
+        const int orow = j - ky;
+        const int slot = ((u - ky) % K + K) % K;
+        const bool live = orow >= 0 && orow < TH;  // uniform
+        if (live) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            float v = ky == 0 ? bd : acc[slot][i];
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) v = fmaf(wk[ky * K + kx], e[i + 2 - P + kx], v);
+            acc[slot][i] = v;
+          }
+        }
+        if (ky == K - 1) finish(orow, acc[slot], live);
+      }
+    }
+  }
+  psum += __shfl_xor(psum, 32, 64);
+  if (h == 0 && chv) atomicAdd(a.pool + (int64_t)n * a.hid + ch, psum);
+}
+
+
+template <int K, int KS>
+int launch_ks(EdArgs a, hipStream_t st) {
+  constexpr int TH = ED4_TH;
+  const int strips = (a.wo + 27) / 28, bands = (a.ho + TH - 1) / TH, ncb = (a.hid + 31) / 32;
+  const int64_t total = (int64_t)ncb * strips * bands * a.n;
+  if (total > 0x7ffffff0LL) return AST_E_SHAPE;
+  const int64_t grid = (total + 7) / 8 * 8;
+  // VEC: wo % 4 == 0, so a 4-column D piece is 8-byte aligned and wholly inside or outside the row
+  if (a.wo % 4 == 0)
+    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, ED4_PD, true>), dim3((unsigned)grid), dim3(64), 0, st, a, strips,
+                       bands, ncb, (int)total);
+  else
+    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, ED4_PD, false>), dim3((unsigned)grid), dim3(64), 0, st, a, strips,
+                       bands, ncb, (int)total);
+  return (int)hipGetLastError();
+}
+
+template <int K>
+int launch_k(EdArgs a, hipStream_t st) {
+  switch (a.cin_pad / 16) {
+    case 1: return launch_ks<K, 1>(a, st);
+    case 2: return launch_ks<K, 2>(a, st);
+    case 3: return launch_ks<K, 3>(a, st);
+    case 4: return launch_ks<K, 4>(a, st);
+    case 5: return launch_ks<K, 5>(a, st);
+    case 6: return launch_ks<K, 6>(a, st);
+    case 8: return launch_ks<K, 8>(a, st);
+    default: return AST_E_UNSUPPORTED;
+  }
+}
+
+}  // namespace
+
+int launch_ed4(EdArgs a, int k, hipStream_t st) {
+  if (a.c1 != a.cin || a.cin_pad % 16 != 0 || (int64_t)a.cin_pad * 2 * a.h * a.w >= 0x7fffffffLL ||
+      (int64_t)a.hid * 2 * a.ho * a.wo >= 0x7fffffffLL)
+    return AST_E_UNSUPPORTED;
+  if (k == 3) return launch_k<3>(a, st);
+  if (k == 5) return launch_k<5>(a, st);
+  return AST_E_UNSUPPORTED;
+}
+
+}  // namespace ast_mb

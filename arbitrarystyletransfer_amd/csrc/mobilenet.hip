@@ -22,6 +22,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include "../../include/ast_hip.h"
+#include "mb_common.h"
 
 namespace {
 
@@ -109,22 +110,7 @@ __device__ __forceinline__ void load8(const bf16* s, float* v) {
 // ------------------------------------------------------------------------------------------------
 // expand + depthwise (+ SE pool sums)
 // ------------------------------------------------------------------------------------------------
-struct EdArgs {
-  const void* x1;
-  const void* x2;   // channels [c1, cin) come from x2 (torch.cat fused away), may equal x1
-  int c1;
-  int n, cin, h, w;  // x geometry (pre-upsample)
-  int hd, wd;        // depthwise input grid (= h*up, w*up)
-  int ho, wo;        // depthwise output
-  const void* w1;    // expand weights T [hid_pad16][cin_pad] (BN folded); null -> ratio-1 block
-  const float* b1;   // [hid]
-  int hid, cin_pad;
-  const float* wdw;  // depthwise weights [hid][k*k] (BN folded)
-  const float* bdw;  // [hid]
-  void* d;           // [n][hid][ho][wo]
-  float* pool;       // [n][hid], accumulated
-  int tiles_x, tiles_y;
-};
+using ast_mb::EdArgs;  // mb_common.h (shared with mb_ed4.hip)
 
 constexpr int kChunk = 16;  // hidden channels per LDS chunk
 
@@ -1498,7 +1484,7 @@ int launch_ed2_auto(EdArgs a, hipStream_t st) {
   return AST_E_UNSUPPORTED;
 }
 
-int g_ed_version = 3;  // AST_MB_ED=1|2 select the v1|v2 kernels (A/B measurements); 3: v3 where it fits
+int g_ed_version = 4;  // AST_MB_ED=1|2|3 select the v1|v2|v3 kernels (A/B measurements); 4: v4 where it applies
 
 int g_ed3_nt = 0;  // AST_MB_ED3_NT=512|1024 forces the v3 workgroup size (A/B measurements)
 
@@ -1525,6 +1511,11 @@ int launch_ed3(EdArgs a, hipStream_t st) {
 
 template <typename T>
 int dispatch_ed(EdArgs a, int k, int s, int up, bool expand, hipStream_t st) {
+  if (sizeof(T) == 2 && s == 1 && up == 1 && expand && g_ed_version >= 4 && a.c1 == a.cin &&
+      (int64_t)a.cin_pad * 2 * a.h * a.w < 0x7fffffffLL) {
+    const int r = ast_mb::launch_ed4(a, k, st);
+    if (r != AST_E_UNSUPPORTED) return r;
+  }
   if (sizeof(T) == 2 && s == 1 && up == 1 && expand && g_ed_version >= 3) {
     const int r = k == 3 ? launch_ed3<3>(a, st) : k == 5 ? launch_ed3<5>(a, st) : AST_E_UNSUPPORTED;
     if (r != AST_E_UNSUPPORTED) return r;
@@ -1608,7 +1599,7 @@ int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, i
   hipStream_t st = (hipStream_t)stream;
   static const int ver = [] {
     const char* v = getenv("AST_MB_ED");
-    return v ? atoi(v) : 3;
+    return v ? atoi(v) : 4;
   }();
   g_ed_version = ver;
   static const int big = [] {
