@@ -54,8 +54,11 @@ __device__ __forceinline__ float hswish_fast(float v) {  // x * clamp(x/6 + 1/2,
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 
-#ifndef ED4_PD
-#define ED4_PD 0  // x rows in flight beyond the next one
+#ifndef ED4_PD3
+#define ED4_PD3 0  // x rows in flight beyond the next one, k = 3
+#endif
+#ifndef ED4_PD5
+#define ED4_PD5 0  // and k = 5
 #endif
 #ifndef ED4_TH
 #define ED4_TH 31  // output rows per band (TH + K - 1 a multiple of K for K = 3, 5)
@@ -240,17 +243,17 @@ __global__ __launch_bounds__(64, (K == 5 && KS >= 6) ? 1 : 2) void expand_dw4_ke
 
 template <int K, int KS>
 int launch_ks(EdArgs a, hipStream_t st) {
-  constexpr int TH = ED4_TH;
+  constexpr int TH = ED4_TH, PD = K == 3 ? ED4_PD3 : ED4_PD5;
   const int strips = (a.wo + 27) / 28, bands = (a.ho + TH - 1) / TH, ncb = (a.hid + 31) / 32;
   const int64_t total = (int64_t)ncb * strips * bands * a.n;
   if (total > 0x7ffffff0LL) return AST_E_SHAPE;
   const int64_t grid = (total + 7) / 8 * 8;
   // VEC: wo % 4 == 0, so a 4-column D piece is 8-byte aligned and wholly inside or outside the row
   if (a.wo % 4 == 0)
-    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, ED4_PD, true>), dim3((unsigned)grid), dim3(64), 0, st, a, strips,
+    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true>), dim3((unsigned)grid), dim3(64), 0, st, a, strips,
                        bands, ncb, (int)total);
   else
-    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, ED4_PD, false>), dim3((unsigned)grid), dim3(64), 0, st, a, strips,
+    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, false>), dim3((unsigned)grid), dim3(64), 0, st, a, strips,
                        bands, ncb, (int)total);
   return (int)hipGetLastError();
 }

@@ -1103,6 +1103,11 @@ struct PwArgs {
   int res_up;
   void* out;
   int tiles;
+  // expand-as-GEMM use (ast_mb_expand_gemm): K channels [c1, hid) come from d2 (the un-materialised
+  // torch.cat), act = 1 applies Hardswish; output channels in slices of MT*16 over gridDim.y
+  const void* d2;
+  int c1;
+  int act;
 };
 
 constexpr int kPwPx = 256;  // pixels per workgroup (4 waves x 64)
@@ -1130,8 +1135,12 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
   const int n = blockIdx.x / a.tiles;
   const int64_t p0 = (int64_t)(blockIdx.x % a.tiles) * kPwPx;
   const int64_t hw = (int64_t)a.h * a.w;
-  const T* dn = reinterpret_cast<const T*>(a.d) + (int64_t)n * a.hid * hw;
-  const T* wn = reinterpret_cast<const T*>(a.wg) + (int64_t)n * a.wg_stride;
+  const int co0 = blockIdx.y * MT * 16;  // output-channel slice (0 for the pw-linear launches)
+  const int cout_l = min(a.cout - co0, MT * 16);
+  // K channel kc of image n: d[n][kc] for kc < c1, else d2[n][kc - c1]
+  const T* dn = reinterpret_cast<const T*>(a.d) + (int64_t)n * a.c1 * hw;
+  const T* dn2 = reinterpret_cast<const T*>(a.d2) + (int64_t)n * (a.hid - a.c1) * hw - (int64_t)a.c1 * hw;
+  const T* wn = reinterpret_cast<const T*>(a.wg) + (int64_t)n * a.wg_stride + (int64_t)co0 * a.hid_pad;
   const bool vec = (hw % VEC) == 0 && p0 + kPwPx <= hw;
 
   constexpr int WV = (MT * 16 * kPwK / VEC + kThreads - 1) / kThreads;
@@ -1145,12 +1154,12 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
       const int e = tid + i * kThreads, c = e / VPR, q = (e % VPR) * VEC;                                  \
       uint4 val = make_uint4(0, 0, 0, 0);                                                                  \
       if (vec) {                                                                                           \
-        if (kb + c < a.hid) val = *reinterpret_cast<const uint4*>(dn + (int64_t)(kb + c) * hw + p0 + q);   \
+        if (kb + c < a.hid) val = *reinterpret_cast<const uint4*>((kb + c < a.c1 ? dn : dn2) + (int64_t)(kb + c) * hw + p0 + q); \
       } else {                                                                                             \
         typename VecOf<T, VEC>::type tv;                                                                   \
         _Pragma("unroll") for (int j = 0; j < VEC; ++j) {                                                  \
           T x = from_f<T>(0.f);                                                                            \
-          if (kb + c < a.hid && p0 + q + j < hw) x = dn[(int64_t)(kb + c) * hw + p0 + q + j];              \
+          if (kb + c < a.hid && p0 + q + j < hw) x = (kb + c < a.c1 ? dn : dn2)[(int64_t)(kb + c) * hw + p0 + q + j]; \
           tv[j] = x;                                                                                       \
         }                                                                                                  \
         val = __builtin_bit_cast(uint4, tv);                                                               \
@@ -1222,8 +1231,9 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
     lds_barrier();
   }
 
-  T* out = reinterpret_cast<T*>(a.out) + (int64_t)n * a.cout * hw;
+  T* out = reinterpret_cast<T*>(a.out) + ((int64_t)n * a.cout + co0) * hw;
   const T* res = reinterpret_cast<const T*>(a.res);
+  const float* bias = a.bias ? a.bias + co0 : nullptr;
   if constexpr (BF) {
     // Whole tile, no upsampled residual: the accumulators go through LDS (16 output channels at a
     // time, fp32, row pitch 260 floats: conflict-free) so every lane stores 8 consecutive pixels
@@ -1234,7 +1244,7 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
       float* st = reinterpret_cast<float*>(ds);
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        if (m * 16 >= a.cout) break;
+        if (m * 16 >= cout_l) break;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -1244,29 +1254,33 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
         for (int i = 0; i < 2; ++i) {
           const int e = tid + i * kThreads, row = e >> 5, q = (e & 31) * 8;  // 16 rows x 32 vectors
           const int co = m * 16 + row;
-          if (co < a.cout) {
+          if (co < cout_l) {
             const f32x4 v0 = *reinterpret_cast<const f32x4*>(st + row * EP + q);
             const f32x4 v1 = *reinterpret_cast<const f32x4*>(st + row * EP + q + 4);
-            const float bco = a.bias ? a.bias[co] : 0.f;
+            const float bco = bias ? bias[co] : 0.f;
             float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
             const int64_t off = (int64_t)co * hw + p0 + q;
             if (res && a.res_up) {  // nearest x2 residual: 4 source pixels, each used twice
               const int pix = (int)(p0 + q), y = pix / a.w, x = pix - y * a.w;
               const int hr = a.h / 2, wr = a.w / 2;
               const uint2 rv = *reinterpret_cast<const uint2*>(
-                  res + (((int64_t)n * a.cout + co) * hr + (y >> 1)) * wr + (x >> 1));
+                  res + (((int64_t)n * a.cout + co0 + co) * hr + (y >> 1)) * wr + (x >> 1));
               typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
               const bf16x4v rb = __builtin_bit_cast(bf16x4v, rv);
 #pragma unroll
               for (int j = 0; j < 8; ++j) v[j] = v[j] + bco + to_f(rb[j >> 1]);
             } else if (res) {
-              const uint4 rv = *reinterpret_cast<const uint4*>(res + (int64_t)n * a.cout * hw + off);
+              const uint4 rv = *reinterpret_cast<const uint4*>(res + ((int64_t)n * a.cout + co0) * hw + off);
               const bf16x8 rb = __builtin_bit_cast(bf16x8, rv);
 #pragma unroll
               for (int j = 0; j < 8; ++j) v[j] = v[j] + bco + to_f(rb[j]);
             } else {
 #pragma unroll
               for (int j = 0; j < 8; ++j) v[j] += bco;
+            }
+            if (a.act) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = hswish(v[j]);
             }
             bf16x8 o;
 #pragma unroll
@@ -1284,8 +1298,8 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int co = m * 16 + 4 * (lane >> 4) + r;
-      if (co >= a.cout) continue;
-      const float bco = a.bias ? a.bias[co] : 0.f;
+      if (co >= cout_l) continue;
+      const float bco = bias ? bias[co] : 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int64_t p = p0 + wave * 64 + t * 16 + (lane & 15);
@@ -1295,11 +1309,12 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
           if (a.res_up) {
             const int pi = (int)p, y = pi / a.w, x = pi - y * a.w;  // p < h*w < 2^31 (host-checked)
             const int hr = a.h / 2, wr = a.w / 2;
-            v += to_f(res[(((int64_t)n * a.cout + co) * hr + (y >> 1)) * wr + (x >> 1)]);
+            v += to_f(res[(((int64_t)n * a.cout + co0 + co) * hr + (y >> 1)) * wr + (x >> 1)]);
           } else {
-            v += to_f(res[((int64_t)n * a.cout + co) * hw + p]);
+            v += to_f(res[((int64_t)n * a.cout + co0 + co) * hw + p]);
           }
         }
+        if (a.act) v = hswish(v);
         out[(int64_t)co * hw + p] = from_f<T>(v);
       }
     }
@@ -1549,7 +1564,8 @@ int dispatch_pw(PwArgs a, hipStream_t st) {
   const int64_t tiles = ((int64_t)a.h * a.w + kPwPx - 1) / kPwPx;
   if ((int64_t)a.n * tiles > 0x7fffffffLL) return AST_E_SHAPE;
   a.tiles = (int)tiles;
-  const dim3 grid((unsigned)(a.n * tiles));
+  const int slices = (a.cout + a.cout_pad - 1) / a.cout_pad;  // 1 for pw-linear
+  const dim3 grid((unsigned)(a.n * tiles), (unsigned)slices);
   switch (mt) {
     case 1: hipLaunchKernelGGL((pw_kernel<T, 1>), grid, dim3(kThreads), 0, st, a); break;
     case 2: hipLaunchKernelGGL((pw_kernel<T, 2>), grid, dim3(kThreads), 0, st, a); break;
@@ -1652,9 +1668,33 @@ int ast_mb_pw(int dtype, const void* d, int n, int hid, int hid_pad, int h, int 
   if (hid_pad < hid || hid_pad % kPwK != 0 || cout_pad < cout || cout_pad % 16 != 0) return AST_E_SHAPE;
   if (res_up && (h % 2 || w % 2)) return AST_E_SHAPE;
   if ((int64_t)h * w >= ((int64_t)1 << 31)) return AST_E_SHAPE;  // 32-bit pixel index in the epilogue
-  PwArgs a{d, n, hid, hid_pad, h, w, wg, (int64_t)wg_stride, bias, cout, cout_pad, res, res_up ? 1 : 0, out, 0};
+  if (cout_pad > 128 || cout > cout_pad) return AST_E_UNSUPPORTED;
+  PwArgs a{d, n, hid, hid_pad, h, w, wg, (int64_t)wg_stride, bias, cout, cout_pad, res, res_up ? 1 : 0, out, 0,
+           d, hid, 0};
   if (dtype == 0) return dispatch_pw<float>(a, (hipStream_t)stream);
   if (dtype == 1) return dispatch_pw<bf16>(a, (hipStream_t)stream);
+  return AST_E_UNSUPPORTED;
+}
+
+int ast_mb_expand_gemm(int dtype, const void* x1, const void* x2, int c1, int n, int cin, int h, int w,
+                       const void* w1p, const float* b1, int hid, int cin_pad, void* out, void* stream) {
+  if (!x1 || !w1p || !b1 || !out) return AST_E_NULLPTR;
+  if (n <= 0 || cin <= 0 || h <= 0 || w <= 0 || hid <= 0) return AST_E_SHAPE;
+  if (!x2) { x2 = x1; c1 = cin; }
+  if (c1 <= 0 || c1 > cin) return AST_E_SHAPE;
+  if (cin_pad < cin || cin_pad % kPwK != 0) return AST_E_SHAPE;
+  if (hid % 128 != 0) return AST_E_UNSUPPORTED;  // whole 128-channel slices: no w1p row past hid is read
+  if ((int64_t)h * w >= ((int64_t)1 << 31)) return AST_E_SHAPE;
+  PwArgs a{x1, n, cin, cin_pad, h, w, w1p, 0, b1, hid, 128, nullptr, 0, out, 0, x2, c1, 1};
+  const hipStream_t st = (hipStream_t)stream;
+  if (dtype == 1) {
+    const int64_t tiles = ((int64_t)h * w + kPwPx - 1) / kPwPx;
+    if ((int64_t)n * tiles > 0x7fffffffLL) return AST_E_SHAPE;
+    a.tiles = (int)tiles;
+    hipLaunchKernelGGL((pw_kernel<bf16, 8>), dim3((unsigned)(n * tiles), (unsigned)((hid + 127) / 128)), dim3(kThreads),
+                       0, st, a);
+    return (int)hipGetLastError();
+  }
   return AST_E_UNSUPPORTED;
 }
 

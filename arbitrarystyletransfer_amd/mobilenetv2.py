@@ -286,11 +286,27 @@ class DepthWiseConv(nn.Module):
         d = torch.empty((n, hid, ho, wo), device=dev, dtype=dt)
         pool = torch.empty((n, hid), device=dev, dtype=torch.float32)
         nb1 = es * (n * cin * h * w + d.numel())
-        check(ops._timed(f"mb expand_dw k{k}s{s}{' up' if up == 2 else ''} {cin}->{hid} {ho}x{wo}", -nb1, dev,
-                         lambda: lib().ast_mb_expand_dw(
-                             DTYPE_CODE[dt], ptr(x), ptr(x2), c1, n, cin, h, w, up, ptr(p.w1p), ptr(p.b1), hid,
-                             p.cin_pad, ptr(p.wd), ptr(p.bd), k, s, ptr(d), ptr(pool), ho, wo, st)),
-              "DepthWiseConv expand+dw")
+        tag = f"mb expand_dw k{k}s{s}{' up' if up == 2 else ''} {cin}->{hid} {ho}x{wo}"
+        if (dt == torch.bfloat16 and p.w1p is not None and p.cin_pad >= 256 and p.cin_pad % 32 == 0
+                and hid % 128 == 0 and s == 1 and up == 1 and k == 3):
+            # too wide for the fused kernels' LDS/registers (ada_out, 256 -> 768): the expand as a GEMM
+            # with Hardswish into a bf16 hidden tensor, then the ratio-1 depthwise pass on it
+            hmid = torch.empty((n, hid, h, w), device=dev, dtype=dt)
+            check(ops._timed(tag + " gemm", -es * (n * cin * h * w + hmid.numel()), dev,
+                             lambda: lib().ast_mb_expand_gemm(
+                                 DTYPE_CODE[dt], ptr(x), ptr(x2), c1, n, cin, h, w, ptr(p.w1p), ptr(p.b1), hid,
+                                 p.cin_pad, ptr(hmid), st)), "DepthWiseConv expand GEMM")
+            check(ops._timed(tag + " dw", -es * (hmid.numel() + d.numel()), dev,
+                             lambda: lib().ast_mb_expand_dw(
+                                 DTYPE_CODE[dt], ptr(hmid), None, hid, n, hid, h, w, 1, None, None, hid, 0,
+                                 ptr(p.wd), ptr(p.bd), k, s, ptr(d), ptr(pool), ho, wo, st)),
+                  "DepthWiseConv dw")
+        else:
+            check(ops._timed(tag, -nb1, dev,
+                             lambda: lib().ast_mb_expand_dw(
+                                 DTYPE_CODE[dt], ptr(x), ptr(x2), c1, n, cin, h, w, up, ptr(p.w1p), ptr(p.b1), hid,
+                                 p.cin_pad, ptr(p.wd), ptr(p.bd), k, s, ptr(d), ptr(pool), ho, wo, st)),
+                  "DepthWiseConv expand+dw")
         wg = torch.empty((n, p.cout_pad, p.hid_pad), device=dev, dtype=dt)
         check(lib().ast_mb_se_fold(DTYPE_CODE[dt], ptr(pool), n, hid, ho * wo, ptr(p.fc1w), ptr(p.fc1b), p.red,
                                    ptr(p.fc2w), ptr(p.fc2b), ptr(p.w2), cout, p.cout_pad, p.hid_pad, ptr(wg), st),

@@ -278,6 +278,14 @@ int ast_mb_pw(int dtype, const void* d, int n, int hid, int hid_pad, int h, int 
               long long wg_stride, const float* bias, int cout, int cout_pad, const void* res,
               int res_up, void* out, void* stream);
 
+/* The expand half of DepthWiseConv (mobilenetv2.py:170-173) on its own, for blocks whose input is
+ * too wide for the fused expand+depthwise kernels (AutoEncoder/AST ada_out, models.py:335: 256 ->
+ * 768): out[n][co] = Hardswish(sum_c w1p[co][c] * cat(x1, x2)[n][c] + b1[co]) in bf16 (dtype 1),
+ * [n][hid][h][w]. The depthwise then runs as the ratio-1 form of ast_mb_expand_dw on out.
+ * cin_pad a multiple of 32, hid a multiple of 128; x2 != NULL feeds channels [c1, cin). */
+int ast_mb_expand_gemm(int dtype, const void* x1, const void* x2, int c1, int n, int cin, int h, int w,
+                       const void* w1p, const float* b1, int hid, int cin_pad, void* out, void* stream);
+
 /* Dense 3x3 reflect-pad convs of the variant: block 0 (conv_3x3_bn, mobilenetv2.py:38-43:
  * cin 3 -> cout 16, no bias, act 1 = Hardswish, fp32 input) and the decoder output conv
  * (models.py:300-316: cin 16 -> cout 3 + bias, fp32 output, act 2 = Hardtanh(0,1) when exporting,
