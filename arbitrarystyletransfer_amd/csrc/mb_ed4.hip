@@ -60,15 +60,23 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 #ifndef ED4_PD5
 #define ED4_PD5 0  // and k = 5
 #endif
+#ifndef ED4_WG4
+#define ED4_WG4 1  // 4-strip workgroups with 16-byte D stores where wo % 8 == 0
+#endif
 #ifndef ED4_TH
 #define ED4_TH 31  // output rows per band (TH + K - 1 a multiple of K for K = 3, 5)
 #endif
 
-template <int K, int KS, int TH, int PD, bool VEC>
-__global__ __launch_bounds__(64, (K == 5 && KS >= 6) ? 1 : 2) void expand_dw4_kernel(EdArgs a, int strips, int bands, int ncb, int total) {
+// WG4 (wo % 8 == 0): a workgroup is 4 waves on 4 adjacent strips (same channel block and band). Their
+// 4 x 28 output columns are contiguous, so each output row goes through one shared LDS image and
+// leaves as 16-byte stores covering 224-byte runs at 16-byte alignment. (Per wave, 56-byte runs of
+// 8-byte stores were store-issue-bound: a build without the D stores ran the k3 blocks 2x faster.)
+template <int K, int KS, int TH, int PD, bool VEC, bool WG4>
+__global__ __launch_bounds__(WG4 ? 256 : 64, (K == 5 && KS >= 6) ? 1 : 2) void expand_dw4_kernel(EdArgs a, int strips, int bands, int ncb, int total) {
   constexpr int P = (K - 1) / 2, NJ = TH + K - 1, OW = 28, SP = 40;  // SP: staging row pitch (bf16)
-  __shared__ __align__(16) bf16 stage[32 * SP];
-  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  constexpr int GP = 4 * OW + 8;  // WG4 staging row pitch (bf16): 240 bytes, 16-byte aligned rows
+  __shared__ __align__(16) bf16 stage[WG4 ? 2 * 32 * GP : 32 * SP];
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wv = WG4 ? threadIdx.x >> 6 : 0;
   // XCD-aware order (workgroup b runs on XCD b % 8): consecutive logical ids -- the channel blocks
   // of one strip, which read the same x -- share an XCD and its L2
   const int per = (total + 7) >> 3;
@@ -76,8 +84,9 @@ __global__ __launch_bounds__(64, (K == 5 && KS >= 6) ? 1 : 2) void expand_dw4_ke
   if (L >= total) return;
   const int cb = L % ncb;
   int rest = L / ncb;
-  const int s = rest % strips;
-  rest /= strips;
+  const int sg = WG4 ? (strips + 3) / 4 : strips;  // strip groups of the grid
+  const int s = WG4 ? 4 * (rest % sg) + wv : rest % sg;
+  rest /= sg;
   const int band = rest % bands;
   const int n = rest / bands;
   const int x0 = s * OW - 2, y0 = band * TH;
@@ -128,6 +137,7 @@ __global__ __launch_bounds__(64, (K == 5 && KS >= 6) ? 1 : 2) void expand_dw4_ke
   constexpr unsigned kDrop = 0x80000000u;
   const bool edge = x0 + 2 + OW > a.wo;  // last strip: outputs past the right border
   float psum = 0.f;
+  int rb = 0;  // WG4 staging image of the next output row
   auto finish = [&](int orow, const float* v, bool live) {
     const int oy = y0 + orow;
     const bool rowv = live && oy < a.ho;  // uniform
@@ -152,6 +162,29 @@ __global__ __launch_bounds__(64, (K == 5 && KS >= 6) ? 1 : 2) void expand_dw4_ke
 #pragma unroll
     for (int i = 0; i < 8; ++i)
       pk[i] = (unsigned)bf16_bits(y[2 * i]) | ((unsigned)bf16_bits(y[2 * i + 1]) << 16);
+    if constexpr (WG4) {
+      // this wave's 14 valid columns per half: local 2..15 (half 0) / 16..29 (half 1) -> image columns
+      // 28 wv + 0..13 / 28 wv + 14..27 of channel row r, in buffer `rb` (a row alternates the two)
+      unsigned* gw = reinterpret_cast<unsigned*>(stage + rb * 32 * GP + r * GP + OW * wv + 14 * h);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) gw[i] = pk[i + 1 - h];
+      lds_barrier();
+      // 32 channel rows x 14 chunks of 8 columns (16 bytes) over the workgroup's 256 threads
+      const int sb = (s - wv) * OW;  // first output column of the workgroup (strip group start)
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const int q = threadIdx.x + 256 * t2;
+        const int cl = min(q / 14, 31), k8 = q - 14 * (q / 14);
+        const uint4 v = *reinterpret_cast<const uint4*>(stage + rb * 32 * GP + cl * GP + 8 * k8);
+        const int xg = sb + 8 * k8;
+        const bool ok = rowv && q < 448 && cb * 32 + cl < a.hid && xg < a.wo;
+        const unsigned off = ok ? (unsigned)(2 * ((cb * 32 + cl) * plane_o + (int64_t)oy * a.wo + xg)) : kDrop;
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, dr, (int)off, 0, 0);
+      }
+      rb ^= 1;  // the other image next row: one barrier per row orders the reuse two rows later
+      return;
+    }
     uint4* sw = reinterpret_cast<uint4*>(stage + r * SP + 16 * h);
     sw[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
     sw[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
@@ -248,13 +281,20 @@ int launch_ks(EdArgs a, hipStream_t st) {
   const int64_t total = (int64_t)ncb * strips * bands * a.n;
   if (total > 0x7ffffff0LL) return AST_E_SHAPE;
   const int64_t grid = (total + 7) / 8 * 8;
-  // VEC: wo % 4 == 0, so a 4-column D piece is 8-byte aligned and wholly inside or outside the row
-  if (a.wo % 4 == 0)
-    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true>), dim3((unsigned)grid), dim3(64), 0, st, a, strips,
-                       bands, ncb, (int)total);
-  else
-    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, false>), dim3((unsigned)grid), dim3(64), 0, st, a, strips,
-                       bands, ncb, (int)total);
+  // WG4 for k = 3 only: measured 3.3 -> 2.9 ms on the 16->96 block at 1024^2, while the k5 blocks
+  // lose 10-50% to the per-row workgroup barrier (their rows are longer and less uniform)
+  if (ED4_WG4 && K == 3 && a.wo % 8 == 0) {  // WG4: 4 strips per workgroup, 16-byte D stores
+    const int64_t total4 = (int64_t)ncb * ((strips + 3) / 4) * bands * a.n, grid4 = (total4 + 7) / 8 * 8;
+    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true, true>), dim3((unsigned)grid4), dim3(256), 0, st, a,
+                       strips, bands, ncb, (int)total4);
+  } else if (a.wo % 4 == 0) {
+    // VEC: wo % 4 == 0, so a 4-column D piece is 8-byte aligned and wholly inside or outside the row
+    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true, false>), dim3((unsigned)grid), dim3(64), 0, st, a,
+                       strips, bands, ncb, (int)total);
+  } else {
+    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, false, false>), dim3((unsigned)grid), dim3(64), 0, st, a,
+                       strips, bands, ncb, (int)total);
+  }
   return (int)hipGetLastError();
 }
 
