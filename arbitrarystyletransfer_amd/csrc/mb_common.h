@@ -24,8 +24,9 @@ struct EdArgs {
   int tiles_x, tiles_y;
 };
 
-// v4 (bf16, stride 1, no upsample, expand blocks with c1 == cin, cin_pad in {16..96, 128}, k in {3, 5}):
-// returns AST_E_UNSUPPORTED when the shape is outside that set (the caller falls back to v3).
-int launch_ed4(EdArgs a, int k, hipStream_t st);
+// v4 (bf16, no upsample, expand blocks with c1 == cin, k in {3, 5}; stride 1 with cin_pad in
+// {16..96, 128}, stride 2 with cin_pad <= 64 and even wo): returns AST_E_UNSUPPORTED when the shape
+// is outside that set (the caller falls back to v3 / v1).
+int launch_ed4(EdArgs a, int k, int stride, hipStream_t st);
 
 }  // namespace ast_mb

@@ -312,12 +312,189 @@ int launch_k(EdArgs a, hipStream_t st) {
   }
 }
 
+
+// Stride 2 (the encoder's down-sampling blocks): the same wave layout -- 32 channels x a strip of 32
+// input columns, expand on the 32x32x16 MFMA, one channel per lane with 16 columns in registers --
+// but a lane makes the outputs at its 8 even local columns, and an input row j feeds the output rows
+// r with j = 2r + ky: S = (K + 1) / 2 rotating accumulators of 8 (static slots by unrolling the row
+// loop by 2S). A strip yields 14 outputs (input local columns 2, 4, .., 28 for k = 3 and 5), a band
+// TH output rows from 2 TH + K - 2 input rows (padded to a multiple of 2S; the extra rows' outputs
+// are dropped). D leaves per output row through LDS as 4-byte pieces (14 columns = 7 dwords per
+// channel row, 4-byte aligned when wo is even).
+template <int K, int KS, int TH>
+__global__ __launch_bounds__(64, 2) void expand_dw4s2_kernel(EdArgs a, int strips, int bands, int ncb, int total) {
+  constexpr int P = (K - 1) / 2, S = (K + 1) / 2, U = 2 * S, NJ0 = 2 * TH + K - 2;
+  constexpr int NJ = (NJ0 + U - 1) / U * U, OW = 14, SP = 16;  // SP: staging row pitch (bf16)
+  __shared__ __align__(16) bf16 stage[32 * SP];
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int per = (total + 7) >> 3;
+  const int L = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (L >= total) return;
+  const int cb = L % ncb;
+  int rest = L / ncb;
+  const int s = rest % strips;
+  rest /= strips;
+  const int band = rest % bands;
+  const int n = rest / bands;
+  const int x0 = 2 * s * OW - 2, y0 = band * TH;  // x0: input column of local 0; y0: first output row
+  const int ch = cb * 32 + r;
+  const bool chv = ch < a.hid;
+
+  float wk[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) wk[i] = chv ? a.wdw[ch * K * K + i] : 0.f;
+  const float bd = chv ? a.bdw[ch] : 0.f, b1 = chv ? a.b1[ch] : 0.f;
+  const int hid16 = (a.hid + 15) / 16 * 16;
+  bf16x8 bw[KS];
+#pragma unroll
+  for (int q = 0; q < KS; ++q)
+    bw[q] = ch < hid16 ? *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.w1) +
+                                                          (int64_t)ch * a.cin_pad + 16 * q + 8 * h)
+                       : bf16x8{};
+  const int pc = 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3);
+  const int gx = refl(x0 + pc, a.wd);
+  const int hw2 = 2 * a.h * a.w;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(reinterpret_cast<const bf16*>(a.x1) + (int64_t)n * a.cin * (hw2 / 2)), 0, a.cin * hw2,
+      0x00020000);
+  unsigned xraw[KS][8];
+  auto load_row = [&](int j) {
+    const int vrow = 8 * h * hw2 + 2 * (refl(2 * y0 - P + j, a.hd) * a.w + gx);
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xraw[q][e] = __builtin_amdgcn_raw_buffer_load_b16(xr, vrow + (16 * q + e) * hw2, 0, 0);
+  };
+
+  const int64_t plane_o = (int64_t)a.ho * a.wo;
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<bf16*>(a.d) + (int64_t)n * a.hid * plane_o, 0, (int)(2 * a.hid * plane_o), 0x00020000);
+  constexpr unsigned kDrop = 0x80000000u;
+  const int oc0 = s * OW;                // first output column of the strip
+  const bool edge = oc0 + OW > a.wo;
+  float psum = 0.f;
+  // this lane's outputs: local input columns 16h + 2i, i = 0..7; valid i = 1..7 (half 0) / 0..6 (half 1),
+  // output columns oc0 + 7h + i - (1 - h)
+  auto finish = [&](int orow, const float* v, bool live) {
+    const int oy = y0 + orow;
+    const bool rowv = live && oy < a.ho;  // uniform
+    float y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) y[i] = hswish_fast(v[i]);
+    float t = 0.f;
+    if (!edge) {
+      t = h ? y[0] : y[7];
+#pragma unroll
+      for (int i = 1; i < 7; ++i) t += y[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int j = 7 * h + i - (1 - h);  // output index within the strip
+        t += (j >= 7 * h && j < 7 * h + 7 && oc0 + j < a.wo) ? y[i] : 0.f;
+      }
+    }
+    psum += rowv ? t : 0.f;
+    unsigned short* sw = reinterpret_cast<unsigned short*>(stage + r * SP + 7 * h);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) sw[i] = bf16_bits(y[i + 1 - h]);
+    lds_barrier();
+#pragma unroll
+    for (int t4 = 0; t4 < 4; ++t4) {
+      const int q = lane + 64 * t4;  // 32 channel rows x 7 dword pieces
+      const int cl = min(q / 7, 31), k2 = q - 7 * (q / 7);
+      const unsigned v0 = *reinterpret_cast<const unsigned*>(stage + cl * SP + 2 * k2);
+      const int xg = oc0 + 2 * k2;
+      const bool ok = rowv && q < 224 && cb * 32 + cl < a.hid && xg < a.wo;
+      const unsigned off = ok ? (unsigned)(2 * ((cb * 32 + cl) * plane_o + (int64_t)oy * a.wo + xg)) : kDrop;
+      __builtin_amdgcn_raw_buffer_store_b32(v0, dr, (int)off, 0, 0);
+    }
+  };
+
+  float acc[S][8];
+  load_row(0);
+  for (int jb = 0; jb < NJ; jb += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = jb + u;
+      f32x16 c;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) c[i] = b1;
+#pragma unroll
+      for (int q = 0; q < KS; ++q) {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f[e] = (xraw[q][2 * e] & 0xffffu) | (xraw[q][2 * e + 1] << 16);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f), bw[q], c, 0, 0, 0);
+      }
+      load_row(j + 1);
+      float e[20];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) e[2 + i] = hswish_fast(c[i]);
+      const float r0 = __shfl_xor(h ? e[2] : e[16], 32, 64), r1 = __shfl_xor(h ? e[3] : e[17], 32, 64);
+      e[0] = r0;
+      e[1] = r1;
+      e[18] = r0;
+      e[19] = r1;
+#pragma unroll
+      for (int ky = K - 1; ky >= 0; --ky) {
+        if ((u - ky) % 2 != 0) continue;  // static: the rows this input row feeds
+        const int orow = (j - ky) / 2;     // j - ky is even
+        const int slot = (((u - ky) / 2) % S + S) % S;
+        const bool live = j - ky >= 0 && orow < TH;
+        if (live) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            float v = ky == 0 ? bd : acc[slot][i];
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) v = fmaf(wk[ky * K + kx], e[2 * i + 2 - P + kx], v);
+            acc[slot][i] = v;
+          }
+        }
+        if (ky == K - 1) finish(orow, acc[slot], live);
+      }
+    }
+  }
+  psum += __shfl_xor(psum, 32, 64);
+  if (h == 0 && chv) atomicAdd(a.pool + (int64_t)n * a.hid + ch, psum);
+}
+
+template <int K, int KS>
+int launch_s2_ks(EdArgs a, hipStream_t st) {
+  constexpr int TH = 32;
+  const int strips = (a.wo + 13) / 14, bands = (a.ho + TH - 1) / TH, ncb = (a.hid + 31) / 32;
+  const int64_t total = (int64_t)ncb * strips * bands * a.n;
+  if (total > 0x7ffffff0LL) return AST_E_SHAPE;
+  const int64_t grid = (total + 7) / 8 * 8;
+  hipLaunchKernelGGL((expand_dw4s2_kernel<K, KS, TH>), dim3((unsigned)grid), dim3(64), 0, st, a, strips, bands, ncb,
+                     (int)total);
+  return (int)hipGetLastError();
+}
+
+template <int K>
+int launch_s2(EdArgs a, hipStream_t st) {
+  switch (a.cin_pad / 16) {
+    case 1: return launch_s2_ks<K, 1>(a, st);
+    case 2: return launch_s2_ks<K, 2>(a, st);
+    case 3: return launch_s2_ks<K, 3>(a, st);
+    case 4: return launch_s2_ks<K, 4>(a, st);
+    default: return AST_E_UNSUPPORTED;
+  }
+}
+
 }  // namespace
 
-int launch_ed4(EdArgs a, int k, hipStream_t st) {
+int launch_ed4(EdArgs a, int k, int stride, hipStream_t st) {
   if (a.c1 != a.cin || a.cin_pad % 16 != 0 || (int64_t)a.cin_pad * 2 * a.h * a.w >= 0x7fffffffLL ||
       (int64_t)a.hid * 2 * a.ho * a.wo >= 0x7fffffffLL)
     return AST_E_UNSUPPORTED;
+  if (a.hd != a.h || a.wd != a.w) return AST_E_UNSUPPORTED;  // no upsample
+  if (stride == 2) {
+    if (a.wo % 2 != 0) return AST_E_UNSUPPORTED;  // 4-byte D pieces
+    if (k == 3) return launch_s2<3>(a, st);
+    if (k == 5) return launch_s2<5>(a, st);
+    return AST_E_UNSUPPORTED;
+  }
   if (k == 3) return launch_k<3>(a, st);
   if (k == 5) return launch_k<5>(a, st);
   return AST_E_UNSUPPORTED;

@@ -55,6 +55,8 @@ BLOCKS = [
     (16, 16, 1, 6, 3, False, True, (1, 3, 5), 1),      # tiny map (reflect pad on 3 rows)
     (20, 20, 1, 6, 3, False, True, (2, 12, 40), 1),    # hidden 120: a partial last 16-channel chunk
     (36, 36, 1, 3, 5, True, True, (1, 19, 70), 1),     # hidden 108, k5, ragged tiles both ways
+    (20, 24, 2, 6, 3, False, True, (2, 70, 92), 1),    # stride 2: hidden 120, 4 strips, odd output height
+    (24, 40, 2, 6, 5, True, True, (1, 66, 124), 1),    # k5 stride 2: 2 bands of output rows, 5 strips
 ]
 
 
