@@ -71,7 +71,12 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 // 4 x 28 output columns are contiguous, so each output row goes through one shared LDS image and
 // leaves as 16-byte stores covering 224-byte runs at 16-byte alignment. (Per wave, 56-byte runs of
 // 8-byte stores were store-issue-bound: a build without the D stores ran the k3 blocks 2x faster.)
-template <int K, int KS, int TH, int PD, bool VEC, bool WG4>
+// R1 (the ratio-1 blocks: DecoderBlock's upsample block, mobilenetv2.py:103-116, and the depthwise
+// pass of the split ada_out): no expand conv -- the MFMA multiplies the block's own 32 channels by
+// an identity B (exact: bf16 x 1.0 accumulated once in fp32), which is the transposition into the
+// lane-per-channel layout; no Hardswish before the depthwise. UP = 2 resolves the nearest upsample
+// in the gather (reflect on the upsampled grid, then halve).
+template <int K, int KS, int TH, int PD, bool VEC, bool WG4, bool R1 = false, int UP = 1>
 __global__ __launch_bounds__(WG4 ? 256 : 64, (K == 5 && KS >= 6) ? 1 : 2) void expand_dw4_kernel(EdArgs a, int strips, int bands, int ncb, int total) {
   constexpr int P = (K - 1) / 2, NJ = TH + K - 1, OW = 28, SP = 40;  // SP: staging row pitch (bf16)
   constexpr int GP = 4 * OW + 8;  // WG4 staging row pitch (bf16): 240 bytes, 16-byte aligned rows
@@ -96,18 +101,24 @@ __global__ __launch_bounds__(WG4 ? 256 : 64, (K == 5 && KS >= 6) ? 1 : 2) void e
   float wk[K * K];
 #pragma unroll
   for (int i = 0; i < K * K; ++i) wk[i] = chv ? a.wdw[ch * K * K + i] : 0.f;
-  const float bd = chv ? a.bdw[ch] : 0.f, b1 = chv ? a.b1[ch] : 0.f;
+  const float bd = chv ? a.bdw[ch] : 0.f, b1 = (chv && !R1) ? a.b1[ch] : 0.f;
   const int hid16 = (a.hid + 15) / 16 * 16;
-  bf16x8 bw[KS];  // B[k = 8h + j][col r] = W1[ch][16 s + 8h + j]
+  bf16x8 bw[KS];  // B[k = 8h + j][col r] = W1[ch][16 s + 8h + j]; R1: identity on the block's channels
 #pragma unroll
-  for (int q = 0; q < KS; ++q)
-    bw[q] = ch < hid16 ? *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.w1) +
-                                                          (int64_t)ch * a.cin_pad + 16 * q + 8 * h)
-                       : bf16x8{};
+  for (int q = 0; q < KS; ++q) {
+    if constexpr (R1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bw[q][j] = (bf16)(16 * q + 8 * h + j == r ? 1.f : 0.f);
+    } else {
+      bw[q] = ch < hid16 ? *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.w1) +
+                                                            (int64_t)ch * a.cin_pad + 16 * q + 8 * h)
+                         : bf16x8{};
+    }
+  }
 
-  // A[row r][k = 8h + j] = x[channel 16 s + 8h + j][pixel pc(r)]
+  // A[row r][k = 8h + j] = x[channel 16 s + 8h + j (+ 32 cb for R1)][pixel pc(r)]
   const int pc = 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3);
-  const int gx = refl(x0 + pc, a.wd);
+  const int gx = refl(x0 + pc, a.wd) / UP;
   const int hw2 = 2 * a.h * a.w;  // bytes per channel plane (host-checked: cin * hw2 < 2^31)
   // one buffer descriptor per image: channels >= cin (the zero-weight padding of the last k-step)
   // fall outside its range and load as 0; x2 is not used (the host takes v4 only for c1 == cin)
@@ -119,7 +130,7 @@ __global__ __launch_bounds__(WG4 ? 256 : 64, (K == 5 && KS >= 6) ? 1 : 2) void e
   // the wave wait for them at once, so no load would overlap the VALU work
   unsigned xraw[PD + 1][KS][8];
   auto load_row = [&](int j, unsigned (*raw)[8]) {
-    const int vrow = 8 * h * hw2 + 2 * (refl(y0 - P + j, a.hd) * a.w + gx);
+    const int vrow = (8 * h + (R1 ? 32 * cb : 0)) * hw2 + 2 * (refl(y0 - P + j, a.hd) / UP * a.w + gx);
 #pragma unroll
     for (int q = 0; q < KS; ++q)
 #pragma unroll
@@ -245,7 +256,7 @@ __global__ __launch_bounds__(WG4 ? 256 : 64, (K == 5 && KS >= 6) ? 1 : 2) void e
       load_row(j + PD + 1, xraw[PD]);  // in flight during this row's VALU work
       float e[20];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) e[2 + i] = hswish_fast(c[i]);
+      for (int i = 0; i < 16; ++i) e[2 + i] = R1 ? c[i] : hswish_fast(c[i]);
       const float r0 = __shfl_xor(h ? e[2] : e[16], 32, 64), r1 = __shfl_xor(h ? e[3] : e[17], 32, 64);
       e[0] = r0;   // half 1: columns 14, 15 (half 0's are never used: its outputs 0, 1 are halo)
       e[1] = r1;
@@ -274,7 +285,7 @@ __global__ __launch_bounds__(WG4 ? 256 : 64, (K == 5 && KS >= 6) ? 1 : 2) void e
 }
 
 
-template <int K, int KS>
+template <int K, int KS, bool R1 = false, int UP = 1>
 int launch_ks(EdArgs a, hipStream_t st) {
   constexpr int TH = ED4_TH, PD = K == 3 ? ED4_PD3 : ED4_PD5;
   const int strips = (a.wo + 27) / 28, bands = (a.ho + TH - 1) / TH, ncb = (a.hid + 31) / 32;
@@ -285,14 +296,14 @@ int launch_ks(EdArgs a, hipStream_t st) {
   // lose 10-50% to the per-row workgroup barrier (their rows are longer and less uniform)
   if (ED4_WG4 && K == 3 && a.wo % 8 == 0) {  // WG4: 4 strips per workgroup, 16-byte D stores
     const int64_t total4 = (int64_t)ncb * ((strips + 3) / 4) * bands * a.n, grid4 = (total4 + 7) / 8 * 8;
-    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true, true>), dim3((unsigned)grid4), dim3(256), 0, st, a,
+    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true, true, R1, UP>), dim3((unsigned)grid4), dim3(256), 0, st, a,
                        strips, bands, ncb, (int)total4);
   } else if (a.wo % 4 == 0) {
     // VEC: wo % 4 == 0, so a 4-column D piece is 8-byte aligned and wholly inside or outside the row
-    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true, false>), dim3((unsigned)grid), dim3(64), 0, st, a,
+    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true, false, R1, UP>), dim3((unsigned)grid), dim3(64), 0, st, a,
                        strips, bands, ncb, (int)total);
   } else {
-    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, false, false>), dim3((unsigned)grid), dim3(64), 0, st, a,
+    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, false, false, R1, UP>), dim3((unsigned)grid), dim3(64), 0, st, a,
                        strips, bands, ncb, (int)total);
   }
   return (int)hipGetLastError();
@@ -485,9 +496,15 @@ int launch_s2(EdArgs a, hipStream_t st) {
 }  // namespace
 
 int launch_ed4(EdArgs a, int k, int stride, hipStream_t st) {
-  if (a.c1 != a.cin || a.cin_pad % 16 != 0 || (int64_t)a.cin_pad * 2 * a.h * a.w >= 0x7fffffffLL ||
+  if (a.c1 != a.cin || (a.w1 && a.cin_pad % 16 != 0) || (int64_t)a.cin_pad * 2 * a.h * a.w >= 0x7fffffffLL ||
       (int64_t)a.hid * 2 * a.ho * a.wo >= 0x7fffffffLL)
     return AST_E_UNSUPPORTED;
+  if (!a.w1) {  // ratio-1 block: k3, stride 1, hid == cin, optional x2 upsample
+    if (k != 3 || stride != 1 || a.hid != a.cin || (int64_t)a.cin * 2 * a.h * a.w >= 0x7fffffffLL) return AST_E_UNSUPPORTED;
+    if (a.hd == 2 * a.h && a.wd == 2 * a.w) return launch_ks<3, 2, true, 2>(a, st);
+    if (a.hd == a.h && a.wd == a.w) return launch_ks<3, 2, true, 1>(a, st);
+    return AST_E_UNSUPPORTED;
+  }
   if (a.hd != a.h || a.wd != a.w) return AST_E_UNSUPPORTED;  // no upsample
   if (stride == 2) {
     if (a.wo % 2 != 0) return AST_E_UNSUPPORTED;  // 4-byte D pieces

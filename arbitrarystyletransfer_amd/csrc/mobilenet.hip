@@ -1526,7 +1526,7 @@ int launch_ed3(EdArgs a, hipStream_t st) {
 
 template <typename T>
 int dispatch_ed(EdArgs a, int k, int s, int up, bool expand, hipStream_t st) {
-  if (sizeof(T) == 2 && up == 1 && expand && g_ed_version >= 4 && a.c1 == a.cin &&
+  if (sizeof(T) == 2 && (up == 1 || !expand) && g_ed_version >= 4 && a.c1 == a.cin &&
       (int64_t)a.cin_pad * 2 * a.h * a.w < 0x7fffffffLL) {
     const int r = ast_mb::launch_ed4(a, k, s, st);
     if (r != AST_E_UNSUPPORTED) return r;
