@@ -61,7 +61,10 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 #define ED4_PD5 0  // and k = 5
 #endif
 #ifndef ED4_WG4
-#define ED4_WG4 1  // 4-strip workgroups with 16-byte D stores where wo % 8 == 0
+#define ED4_WG4 1  // multi-strip workgroups with 16-byte D stores where wo % 8 == 0
+#endif
+#ifndef ED4_WGN
+#define ED4_WGN 4  // strips (waves) per such workgroup (even)
 #endif
 #ifndef ED4_TH
 #define ED4_TH 31  // output rows per band (TH + K - 1 a multiple of K for K = 3, 5)
@@ -77,9 +80,10 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 // lane-per-channel layout; no Hardswish before the depthwise. UP = 2 resolves the nearest upsample
 // in the gather (reflect on the upsampled grid, then halve).
 template <int K, int KS, int TH, int PD, bool VEC, bool WG4, bool R1 = false, int UP = 1>
-__global__ __launch_bounds__(WG4 ? 256 : 64, (K == 5 && KS >= 6) ? 1 : 2) void expand_dw4_kernel(EdArgs a, int strips, int bands, int ncb, int total) {
+__global__ __launch_bounds__(WG4 ? 64 * ED4_WGN : 64, (K == 5 && KS >= 6) ? 1 : 2) void expand_dw4_kernel(EdArgs a, int strips, int bands, int ncb, int total) {
   constexpr int P = (K - 1) / 2, NJ = TH + K - 1, OW = 28, SP = 40;  // SP: staging row pitch (bf16)
-  constexpr int GP = 4 * OW + 8;  // WG4 staging row pitch (bf16): 240 bytes, 16-byte aligned rows
+  constexpr int NW = ED4_WGN, CPR = NW * OW / 8;  // WG4: strips per workgroup, 16-byte chunks per row
+  constexpr int GP = NW * OW + 8;  // WG4 staging row pitch (bf16): 16-byte aligned rows
   __shared__ __align__(16) bf16 stage[WG4 ? 2 * 32 * GP : 32 * SP];
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wv = WG4 ? threadIdx.x >> 6 : 0;
   // XCD-aware order (workgroup b runs on XCD b % 8): consecutive logical ids -- the channel blocks
@@ -89,8 +93,8 @@ __global__ __launch_bounds__(WG4 ? 256 : 64, (K == 5 && KS >= 6) ? 1 : 2) void e
   if (L >= total) return;
   const int cb = L % ncb;
   int rest = L / ncb;
-  const int sg = WG4 ? (strips + 3) / 4 : strips;  // strip groups of the grid
-  const int s = WG4 ? 4 * (rest % sg) + wv : rest % sg;
+  const int sg = WG4 ? (strips + NW - 1) / NW : strips;  // strip groups of the grid
+  const int s = WG4 ? NW * (rest % sg) + wv : rest % sg;
   rest /= sg;
   const int band = rest % bands;
   const int n = rest / bands;
@@ -184,11 +188,11 @@ __global__ __launch_bounds__(WG4 ? 256 : 64, (K == 5 && KS >= 6) ? 1 : 2) void e
       const int sb = (s - wv) * OW;  // first output column of the workgroup (strip group start)
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2) {
-        const int q = threadIdx.x + 256 * t2;
-        const int cl = min(q / 14, 31), k8 = q - 14 * (q / 14);
+        const int q = threadIdx.x + 64 * NW * t2;
+        const int cl = min(q / CPR, 31), k8 = q - CPR * (q / CPR);
         const uint4 v = *reinterpret_cast<const uint4*>(stage + rb * 32 * GP + cl * GP + 8 * k8);
         const int xg = sb + 8 * k8;
-        const bool ok = rowv && q < 448 && cb * 32 + cl < a.hid && xg < a.wo;
+        const bool ok = rowv && q < 32 * CPR && cb * 32 + cl < a.hid && xg < a.wo;
         const unsigned off = ok ? (unsigned)(2 * ((cb * 32 + cl) * plane_o + (int64_t)oy * a.wo + xg)) : kDrop;
         typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, dr, (int)off, 0, 0);
@@ -295,8 +299,8 @@ int launch_ks(EdArgs a, hipStream_t st) {
   // WG4 for k = 3 only: measured 3.3 -> 2.9 ms on the 16->96 block at 1024^2, while the k5 blocks
   // lose 10-50% to the per-row workgroup barrier (their rows are longer and less uniform)
   if (ED4_WG4 && K == 3 && a.wo % 8 == 0) {  // WG4: 4 strips per workgroup, 16-byte D stores
-    const int64_t total4 = (int64_t)ncb * ((strips + 3) / 4) * bands * a.n, grid4 = (total4 + 7) / 8 * 8;
-    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true, true, R1, UP>), dim3((unsigned)grid4), dim3(256), 0, st, a,
+    const int64_t total4 = (int64_t)ncb * ((strips + ED4_WGN - 1) / ED4_WGN) * bands * a.n, grid4 = (total4 + 7) / 8 * 8;
+    hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true, true, R1, UP>), dim3((unsigned)grid4), dim3(64 * ED4_WGN), 0, st, a,
                        strips, bands, ncb, (int)total4);
   } else if (a.wo % 4 == 0) {
     // VEC: wo % 4 == 0, so a 4-column D piece is 8-byte aligned and wholly inside or outside the row
@@ -506,6 +510,10 @@ int launch_ed4(EdArgs a, int k, int stride, hipStream_t st) {
     return AST_E_UNSUPPORTED;
   }
   if (a.hd != a.h || a.wd != a.w) return AST_E_UNSUPPORTED;  // no upsample
+  // k3 with wide inputs on small maps (128^2 and below: 128->384, 96->288, 80->320 in config 5)
+  // measured faster on v3 (0.48 vs 0.59 ms for 128->384): the 28-column strips waste 9% of a
+  // 128-column map and the grid is a few waves deep
+  if (k == 3 && stride == 1 && a.cin_pad >= 80 && (int64_t)a.ho * a.wo <= 128 * 128) return AST_E_UNSUPPORTED;
   if (stride == 2) {
     if (a.wo % 2 != 0) return AST_E_UNSUPPORTED;  // 4-byte D pieces
     if (k == 3) return launch_s2<3>(a, st);
