@@ -1111,6 +1111,9 @@ struct PwArgs {
 };
 
 constexpr int kPwPx = 256;  // pixels per workgroup (4 waves x 64)
+#ifndef PW_PX_BF16
+#define PW_PX_BF16 256  // bf16 pw with <= 48 output channels: pixels per workgroup (256 | 512)
+#endif
 constexpr int kPwK = 32;    // hidden channels per LDS stage
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -1121,19 +1124,20 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 // transposed read ds_read_b64_tr_b16 delivers from that layout; the MFMA k order is permuted to
 // (4g..4g+3, 16+4g..16+4g+3) for lane group g (A uses the same order), so each half-wave's read
 // touches 8 consecutive rows, conflict-free with a row pitch of 16 (mod 128) elements.
-template <typename T, int MT>
+template <typename T, int MT, int PX = kPwPx>
 __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
+  constexpr int TT = PX / 64;  // 16-pixel MFMA tiles per wave
   constexpr bool BF = sizeof(T) == 2;
-  constexpr int LDP = kPwPx + (BF ? 16 : 4);     // D image row pitch (elements)
+  constexpr int LDP = PX + (BF ? 16 : 4);     // D image row pitch (elements)
   constexpr int LDW = kPwK + Mma<T>::PAD;        // weight image row pitch
   constexpr int VEC = 16 / sizeof(T);            // elements per 16-byte vector
-  constexpr int NV = kPwK * kPwPx / VEC / kThreads;
-  constexpr int VPR = kPwPx / VEC;               // vectors per channel row
+  constexpr int NV = kPwK * PX / VEC / kThreads;
+  constexpr int VPR = PX / VEC;               // vectors per channel row
   __shared__ __align__(16) T ds[kPwK * LDP];
   __shared__ __align__(16) T ws[MT * 16 * LDW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = blockIdx.x / a.tiles;
-  const int64_t p0 = (int64_t)(blockIdx.x % a.tiles) * kPwPx;
+  const int64_t p0 = (int64_t)(blockIdx.x % a.tiles) * PX;
   const int64_t hw = (int64_t)a.h * a.w;
   const int co0 = blockIdx.y * MT * 16;  // output-channel slice (0 for the pw-linear launches)
   const int cout_l = min(a.cout - co0, MT * 16);
@@ -1141,7 +1145,7 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
   const T* dn = reinterpret_cast<const T*>(a.d) + (int64_t)n * a.c1 * hw;
   const T* dn2 = reinterpret_cast<const T*>(a.d2) + (int64_t)n * (a.hid - a.c1) * hw - (int64_t)a.c1 * hw;
   const T* wn = reinterpret_cast<const T*>(a.wg) + (int64_t)n * a.wg_stride + (int64_t)co0 * a.hid_pad;
-  const bool vec = (hw % VEC) == 0 && p0 + kPwPx <= hw;
+  const bool vec = (hw % VEC) == 0 && p0 + PX <= hw;
 
   constexpr int WV = (MT * 16 * kPwK / VEC + kThreads - 1) / kThreads;
   uint4 pre[NV];  // next chunk of D, prefetched into registers
@@ -1174,11 +1178,11 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
     }                                                                                                      \
   }
 
-  f32x4 acc[MT][4];
+  f32x4 acc[MT][TT];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < TT; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   PW_FETCH(0);
   for (int k0 = 0; k0 < a.hid_pad; k0 += kPwK) {
@@ -1196,10 +1200,10 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
     if (k0 + kPwK < a.hid_pad) PW_FETCH(k0 + kPwK);  // in flight during the MFMAs and across the barrier
     if constexpr (BF) {
       const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-      bf16x8 bfr[4];
+      bf16x8 bfr[TT];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int col = wave * 64 + t * 16 + 4 * p;
+      for (int t = 0; t < TT; ++t) {
+        const int col = wave * (PX / 4) + t * 16 + 4 * p;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds + (4 * g + q) * LDP + col));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds + (16 + 4 * g + q) * LDP + col));
         bfr[t] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
@@ -1211,20 +1215,20 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
         const s16x4 hi = *reinterpret_cast<const s16x4*>(wr + 16);
         const bf16x8 afr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[t], acc[m][t], 0, 0, 0);
+        for (int t = 0; t < TT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[t], acc[m][t], 0, 0, 0);
       }
     } else {
 #pragma unroll
       for (int ks = 0; ks < kPwK; ks += 4) {
         const int kr = ks + (lane >> 4);
-        float bfr[4];
+        float bfr[TT];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) bfr[t] = ds[kr * LDP + wave * 64 + t * 16 + (lane & 15)];
+        for (int t = 0; t < TT; ++t) bfr[t] = ds[kr * LDP + wave * (PX / 4) + t * 16 + (lane & 15)];
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           const float afr = ws[(m * 16 + (lane & 15)) * LDW + kr];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(afr, bfr[t], acc[m][t], 0, 0, 0);
+          for (int t = 0; t < TT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(afr, bfr[t], acc[m][t], 0, 0, 0);
         }
       }
     }
@@ -1238,7 +1242,7 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
     // Whole tile, no upsampled residual: the accumulators go through LDS (16 output channels at a
     // time, fp32, row pitch 260 floats: conflict-free) so every lane stores 8 consecutive pixels
     // with one 16-byte write (the direct epilogue's 2-byte stores cover 32-byte runs only).
-    constexpr int EP = kPwPx + 4;
+    constexpr int EP = PX + 4;
     static_assert(16 * EP * sizeof(float) <= sizeof(ds), "epilogue staging fits the D image");
     if (vec && (hw % 8) == 0 && (!a.res_up || (a.w % 8) == 0)) {
       float* st = reinterpret_cast<float*>(ds);
@@ -1248,11 +1252,11 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) st[(4 * (lane >> 4) + r) * EP + wave * 64 + t * 16 + (lane & 15)] = acc[m][t][r];
+          for (int t = 0; t < TT; ++t) st[(4 * (lane >> 4) + r) * EP + wave * (PX / 4) + t * 16 + (lane & 15)] = acc[m][t][r];
         lds_barrier();
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int e = tid + i * kThreads, row = e >> 5, q = (e & 31) * 8;  // 16 rows x 32 vectors
+        for (int i = 0; i < 2 * PX / 256; ++i) {
+          const int e = tid + i * kThreads, row = e / (PX / 8), q = (e % (PX / 8)) * 8;  // 16 rows x PX/8 vectors
           const int co = m * 16 + row;
           if (co < cout_l) {
             const f32x4 v0 = *reinterpret_cast<const f32x4*>(st + row * EP + q);
@@ -1301,8 +1305,8 @@ __global__ __launch_bounds__(kThreads, 2) void pw_kernel(PwArgs a) {
       if (co >= cout_l) continue;
       const float bco = bias ? bias[co] : 0.f;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int64_t p = p0 + wave * 64 + t * 16 + (lane & 15);
+      for (int t = 0; t < TT; ++t) {
+        const int64_t p = p0 + wave * (PX / 4) + t * 16 + (lane & 15);
         if (p >= hw) continue;
         float v = acc[m][t][r] + bco;
         if (res) {
@@ -1561,15 +1565,17 @@ int dispatch_ed(EdArgs a, int k, int s, int up, bool expand, hipStream_t st) {
 template <typename T>
 int dispatch_pw(PwArgs a, hipStream_t st) {
   const int mt = a.cout_pad / 16;
-  const int64_t tiles = ((int64_t)a.h * a.w + kPwPx - 1) / kPwPx;
+  constexpr int PXB = sizeof(T) == 2 ? PW_PX_BF16 : kPwPx;  // pixels per workgroup, MT <= 3
+  const int px = mt <= 3 ? PXB : kPwPx;
+  const int64_t tiles = ((int64_t)a.h * a.w + px - 1) / px;
   if ((int64_t)a.n * tiles > 0x7fffffffLL) return AST_E_SHAPE;
   a.tiles = (int)tiles;
   const int slices = (a.cout + a.cout_pad - 1) / a.cout_pad;  // 1 for pw-linear
   const dim3 grid((unsigned)(a.n * tiles), (unsigned)slices);
   switch (mt) {
-    case 1: hipLaunchKernelGGL((pw_kernel<T, 1>), grid, dim3(kThreads), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((pw_kernel<T, 2>), grid, dim3(kThreads), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((pw_kernel<T, 3>), grid, dim3(kThreads), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((pw_kernel<T, 1, PXB>), grid, dim3(kThreads), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((pw_kernel<T, 2, PXB>), grid, dim3(kThreads), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((pw_kernel<T, 3, PXB>), grid, dim3(kThreads), 0, st, a); break;
     case 4: hipLaunchKernelGGL((pw_kernel<T, 4>), grid, dim3(kThreads), 0, st, a); break;
     case 5: hipLaunchKernelGGL((pw_kernel<T, 5>), grid, dim3(kThreads), 0, st, a); break;
     case 6: hipLaunchKernelGGL((pw_kernel<T, 6>), grid, dim3(kThreads), 0, st, a); break;
