@@ -1403,13 +1403,18 @@ __device__ __forceinline__ void load8f(const T* p, float* v) {
   }
 }
 
-template <typename TI, typename TO, int CIN, int COUT, int ACT>
+template <typename TI, typename TO, int CIN, int COUT_ALL, int ACT, int CB = COUT_ALL>
 __global__ __launch_bounds__(kThreads) void dense3x3v8_kernel(const TI* __restrict__ x, const float* __restrict__ wt,
                                                               const float* __restrict__ bias, TO* __restrict__ y,
                                                               int h, int w, int64_t groups_per_image, int64_t total) {
+  // CB output channels per thread: blockIdx.y selects the block of channels (block 0's 16 channels
+  // as two blocks of 8 keep the accumulators at 64 registers)
+  constexpr int COUT = CB;
   __shared__ float wsm[COUT * CIN * 9];
-  for (int i = threadIdx.x; i < COUT * CIN * 9; i += kThreads) wsm[i] = wt[i];
+  const int cb0 = blockIdx.y * CB;
+  for (int i = threadIdx.x; i < COUT * CIN * 9; i += kThreads) wsm[i] = wt[cb0 * CIN * 9 + i];
   __syncthreads();
+  if (bias) bias += cb0;
   const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;  // 8-pixel group
   if (g >= total) return;
   const int64_t n = g / groups_per_image;
@@ -1445,7 +1450,7 @@ __global__ __launch_bounds__(kThreads) void dense3x3v8_kernel(const TI* __restri
   }
 #pragma unroll
   for (int co = 0; co < COUT; ++co) {
-    TO* o = y + (n * COUT + co) * hw + (int64_t)oy * w + ox0;
+    TO* o = y + (n * COUT_ALL + cb0 + co) * hw + (int64_t)oy * w + ox0;
     float v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -1665,14 +1670,16 @@ int dispatch_pw(PwArgs a, hipStream_t st) {
 
 template <typename TI, typename TO, int CIN, int COUT, int ACT>
 int launch_dense(const void* x, const float* w, const float* b, void* y, int n, int h, int wd, hipStream_t st) {
-  // whole 8-pixel groups, 16-byte aligned rows; few output channels only (16 channels x 8 pixels of
+  // whole 8-pixel groups, 16-byte aligned rows; at most 8 output channels per thread (16 x 8 pixels of
   // accumulators would leave one wave per SIMD)
-  if (COUT <= 8 && wd % 8 == 0 && wd >= 16) {
+  if (wd % 8 == 0 && wd >= 16) {
+    constexpr int CB = COUT <= 8 ? COUT : 8;
+    static_assert(COUT % CB == 0, "whole channel blocks");
     const int64_t gpi = (int64_t)h * (wd / 8);
     const int64_t blocks = (n * gpi + kThreads - 1) / kThreads;
     if (blocks > 0x7fffffffLL) return AST_E_SHAPE;
-    hipLaunchKernelGGL((dense3x3v8_kernel<TI, TO, CIN, COUT, ACT>), dim3((unsigned)blocks), dim3(kThreads), 0, st,
-                       reinterpret_cast<const TI*>(x), w, b, reinterpret_cast<TO*>(y), h, wd, gpi, n * gpi);
+    hipLaunchKernelGGL((dense3x3v8_kernel<TI, TO, CIN, COUT, ACT, CB>), dim3((unsigned)blocks, COUT / CB), dim3(kThreads),
+                       0, st, reinterpret_cast<const TI*>(x), w, b, reinterpret_cast<TO*>(y), h, wd, gpi, n * gpi);
     return (int)hipGetLastError();
   }
   const int64_t gpi = (int64_t)h * ((wd + 3) / 4);

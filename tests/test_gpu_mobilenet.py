@@ -105,11 +105,12 @@ def test_ada_out_split_input_matches_cat(dtype, hip_device):
     assert rel_inf(y_split, ref) <= (BLOCK_TOL if dtype == torch.float32 else BF16_BLOCK_TOL)
 
 
-@pytest.mark.parametrize("fshape", [(2, 16, 9, 14), (2, 16, 7, 32)])   # 4-pixel kernel / 8-pixel kernel
-def test_dense_convs(fshape, hip_device):
+@pytest.mark.parametrize("xshape,fshape", [((2, 3, 17, 30), (2, 16, 9, 14)),    # 4-pixel kernel
+                                           ((2, 3, 13, 40), (2, 16, 7, 32))])   # 8-pixel kernel
+def test_dense_convs(xshape, fshape, hip_device):
     enc = synth.live_init_(models.Encoder(), 5).eval().to(hip_device)
     dec = synth.live_init_(models.Decoder(), 6).eval().to(hip_device)
-    x = torch.from_numpy(synth.image(41, (2, 3, 17, 30)))
+    x = torch.from_numpy(synth.image(41, xshape))
     f = torch.from_numpy(synth.image(42, fshape) - 0.5)
     with torch.no_grad():
         y0 = enc.mob_net[0](x.to(hip_device))
