@@ -23,6 +23,7 @@ _d = ctypes.c_double
 # name -> (restype, argtypes); must match include/ast_hip.h exactly (tests/test_capi.py checks it)
 SIGNATURES = {
     "ast_version": (ctypes.c_char_p, []),
+    "ast_loss_acc_floats": (_i, []),
     "ast_conv3x3_packed_numel": (ctypes.c_size_t, [_i, _i]),
     "ast_conv3x3_pack_weights_f32": (_i, [_p, _p, _i, _i, _p]),
     "ast_conv3x3_pack_split_f32": (_i, [_p, _i, _i, _p]),
@@ -39,9 +40,11 @@ SIGNATURES = {
     "ast_relu_mask_f32": (_i, [_p, _p, _p, _ll, _p]),
     "ast_grad_pad_f32": (_i, [_p, _p, _p, _ll, _i, _i, _i, _p]),
     "ast_pad_up_adjoint_f32": (_i, [_p, _p, _ll, _i, _i, _i, _i, _p]),
-    "ast_conv3x3_wgrad_f32": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
-    "ast_conv3x3_wgrad_ex_f32": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _ll, _ll, _p]),
-    "ast_gram_f32": (_i, [_p, _p, _i, _i, _ll, _f, _p]),
+    "ast_conv3x3_wgrad_workspace_floats": (_ll, [_i, _i, _i, _i, _i, _i]),
+    "ast_conv3x3_wgrad_f32": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _ll, _p]),
+    "ast_conv3x3_wgrad_ex_f32": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _ll, _ll, _p, _ll, _p]),
+    "ast_gram_workspace_floats": (_ll, [_i, _i, _ll]),
+    "ast_gram_f32": (_i, [_p, _p, _i, _i, _ll, _f, _p, _ll, _p]),
     "ast_gram_backward_f32": (_i, [_p, _p, _p, _p, _p, _i, _i, _ll, _f, _p, _i, _p]),
     "ast_mvn_huber_f32": (_i, [_p, _p, _ll, _ll, _f, _p, _p, _p]),
     "ast_mvn_huber_backward_f32": (_i, [_p, _p, _p, _ll, _ll, _f, _p, _p, _i, _p]),
@@ -56,8 +59,9 @@ SIGNATURES = {
     "ast_grad_norm_f32": (_i, [_p, _i, _ll, _p, _f, _p, _p]),
     "ast_grad_scale_f32": (_i, [_p, _i, _ll, _p, _p]),
     "ast_adam_step_f32": (_i, [_p, _i, _ll, _p, _d, _d, _d, _d, _i, _p]),
+    "ast_mb_expand_dw_workspace_floats": (_ll, [_i] * 15),
     "ast_mb_expand_dw": (_i, [_i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p,
-                              _i, _i, _p]),
+                              _i, _i, _p, _ll, _p]),
     "ast_mb_se_fold": (_i, [_i, _p, _i, _i, _ll, _p, _p, _i, _p, _p, _p, _i, _i, _i, _p, _p]),
     "ast_mb_pw": (_i, [_i, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _i, _i, _p, _i, _p, _p]),
     "ast_mb_expand_gemm": (_i, [_i, _p, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p]),
@@ -72,7 +76,8 @@ SIGNATURES = {
     "ast_fma_inplace_f32": (_i, [_p, _p, _p, _ll, _p]),
     "ast_adaattn_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i, _i, _i, _i]),
     "ast_adaattn_fwd": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, ctypes.c_size_t, _i, _i, _i, _i, _i, _i, _p]),
-    "ast_soft_hist_f32": (_i, [_p, _i, _ll, _f, _p, _p]),
+    "ast_soft_hist_workspace_floats": (_ll, [_i]),
+    "ast_soft_hist_f32": (_i, [_p, _i, _ll, _f, _p, _p, _ll, _p]),
     "ast_emd_loss_f32": (_i, [_p, _p, _i, _f, _p, _p, _p, _p]),
     "ast_soft_hist_backward_f32": (_i, [_p, _i, _ll, _f, _p, _p, _i, _p]),
     "ast_range_loss_f32": (_i, [_p, _ll, _f, _p, _p, _p, _i, _p]),
@@ -86,8 +91,9 @@ SIGNATURES = {
     "ast_aug_blur_f32": (_i, [_p, _i, _i, _i, _p, _i, _p, _p, _p]),
     "ast_pack_images_f32": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _i, _p, _p]),
     "ast_unpack_images_f32": (_i, [_p, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
-    "ast_mbt_gemm_f32": (_i, [_p, _p, _p, _i, _i, _i, _i, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _i, _i, _i, _i, _i,
-                              _p]),
+    "ast_mbt_gemm_workspace_floats": (_ll, [_i, _i, _i, _i, _ll]),
+    "ast_mbt_gemm_f32": (_i, [_p, _p, _p, _i, _i, _i, _i, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _ll, _i, _i, _i, _i, _p,
+                              _ll, _p]),
     "ast_mbt_dw_workspace_floats": (_ll, [_i, _i, _i, _i, _i]),
     "ast_mbt_dw_f32": (_i, [_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _ll, _p]),
     "ast_mbt_bn_workspace_floats": (_ll, [_i, _i, _ll]),
@@ -101,7 +107,7 @@ SIGNATURES = {
     "ast_mbt_eltwise_f32": (_i, [_i, _p, _p, _p, _ll, _i, _i, _p]),
     "ast_mbt_plane_f32": (_i, [_i, _p, _p, _p, _p, _p, _ll, _ll, _p]),
     "ast_mbt_se_fc_fwd_f32": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p]),
-    "ast_mbt_se_fc_bwd_f32": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _ll, _p, _p, _p, _p, _p, _p]),
+    "ast_mbt_se_fc_bwd_f32": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _ll, _p, _p, _p, _p, _p, _p, _ll, _p]),
 }
 
 ERRORS = {-1: "null pointer", -2: "bad shape", -3: "unsupported configuration"}
@@ -142,3 +148,20 @@ def stream_ptr(device: torch.device) -> int:
 
 def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+def workspace(nfloats: int, device) -> "torch.Tensor":
+    """Device scratch of a deterministic reduction (the *_workspace_floats queries of ast_hip.h):
+    taken from the caching allocator per call, so stream order alone keeps calls apart."""
+    return torch.empty((max(1, int(nfloats)),), device=device, dtype=torch.float32)
+
+
+_ACC_FLOATS = None
+
+
+def loss_accumulator(device) -> "torch.Tensor":
+    """A zeroed loss accumulator (AST_LOSS_ACC_FLOATS floats; the value is element 0)."""
+    global _ACC_FLOATS
+    if _ACC_FLOATS is None:
+        _ACC_FLOATS = int(lib().ast_loss_acc_floats())
+    return torch.zeros((_ACC_FLOATS,), device=device, dtype=torch.float32)

@@ -8,7 +8,7 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import HipOpError, check, lib, ptr, stream_ptr
+from ._lib import HipOpError, check, lib, loss_accumulator, ptr, stream_ptr
 
 COLOR_OPS = {"brightness": 0, "contrast": 1, "saturation": 2, "hue": 3, "grayscale": 4}
 
@@ -86,7 +86,7 @@ def adjust_brightness(img, f):
 
 def adjust_contrast(img, f):
     img = _img(img)
-    gsum = torch.empty((1,), device=img.device, dtype=torch.float32)
+    gsum = loss_accumulator(img.device)   # the sum lands in element 0 (fixed-order reduction)
     check(lib().ast_aug_gray_sum_f32(ptr(img), img.shape[1], img.shape[2], ptr(gsum), stream_ptr(img.device)),
           "gray_sum")
     return _color(img, "contrast", f, gsum)

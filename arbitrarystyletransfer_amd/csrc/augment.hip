@@ -16,6 +16,7 @@
 #include <math.h>
 #include <stdint.h>
 #include "../../include/ast_hip.h"
+#include "det.h"
 
 namespace {
 
@@ -52,7 +53,7 @@ __global__ void remap_kernel(const float* __restrict__ src, int c, int hi, int w
 __device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
 __device__ __forceinline__ float gray(float r, float g, float b) { return 0.2989f * r + 0.587f * g + 0.114f * b; }
 
-// sum of rgb_to_grayscale over an image (for adjust_contrast's mean), accumulated into *acc
+// sum of rgb_to_grayscale over an image (for adjust_contrast's mean), into the accumulator acc (det.h)
 __global__ void gray_sum_kernel(const float* __restrict__ img, int64_t hw, float* acc) {
   __shared__ float sh[kThreads / 64];
   float s = 0.f;
@@ -62,7 +63,7 @@ __global__ void gray_sum_kernel(const float* __restrict__ img, int64_t hw, float
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(acc, (sh[0] + sh[1]) + (sh[2] + sh[3]));
+  ast_det::loss_acc_commit(acc, (sh[0] + sh[1]) + (sh[2] + sh[3]));  // fixed-order sum over workgroups
 }
 
 // op: 0 brightness, 1 contrast (mean = *gsum / hw), 2 saturation, 3 hue, 4 grayscale (3 channels)

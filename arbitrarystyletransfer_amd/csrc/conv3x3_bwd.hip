@@ -19,6 +19,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include "../../include/ast_hip.h"
+#include "det.h"
 
 namespace {
 
@@ -173,8 +174,8 @@ struct WgCfg {
 struct WgArgs {
   const float* x;
   const float* dy;
-  float* dw;
-  float* db;
+  float* dw;  // partials: split s writes its dW tile into dw + s * Cout * Cin * 9 (the workspace)
+  float* db;  // and its db into db + s * Cout (workspace; null: no bias)
   int N, Cin, Hin, Win, Cout, reflect;
   int dy_pitch;        // row stride of dy
   int64_t dy_plane;    // plane stride of dy
@@ -295,17 +296,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgArgs a) {
   }
   // C[i = co][j = ci]: col j = l32, rows i = (r&3)+8(r>>2)+4h
   const int ci = ci0 + wci * 32 + l32;
+  float* const dwp = a.dw + (int64_t)split * a.Cout * a.Cin * 9;
   if (ci < a.Cin) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (co < a.Cout) atomicAdd(a.dw + ((int64_t)co * a.Cin + ci) * 9 + t, acc[t][r]);
+        if (co < a.Cout) dwp[((int64_t)co * a.Cin + ci) * 9 + t] = acc[t][r];
       }
     }
   }
-  if (a.db && cig == 0 && co0 + (tid & 63) < a.Cout) atomicAdd(a.db + co0 + (tid & 63), bacc);
+  if (a.db && cig == 0 && co0 + (tid & 63) < a.Cout) a.db[split * a.Cout + co0 + (tid & 63)] = bacc;
 }
 
 // Weight gradient for Cout <= 4 (the decoders' image convs, models.py:627), or Cout <= 16 with
@@ -403,9 +405,9 @@ __global__ __launch_bounds__(256) void wgrad_smallco_kernel(WgArgs a) {
     const float v = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
     if (e < COUT * SC_CG * 9) {
       const int o = e / (SC_CG * 9), t = e % (SC_CG * 9), c = t / 9, tap = t % 9;
-      if (o < a.Cout && ci0 + c < a.Cin) atomicAdd(a.dw + ((int64_t)o * a.Cin + ci0 + c) * 9 + tap, v);
+      if (o < a.Cout && ci0 + c < a.Cin) a.dw[split * a.Cout * a.Cin * 9 + ((int64_t)o * a.Cin + ci0 + c) * 9 + tap] = v;
     } else if (a.db && cig == 0 && e - COUT * SC_CG * 9 < a.Cout) {
-      atomicAdd(a.db + (e - COUT * SC_CG * 9), v);
+      a.db[split * a.Cout + (e - COUT * SC_CG * 9)] = v;
     }
   }
 }
@@ -534,14 +536,15 @@ __global__ __launch_bounds__(256, 2) void wgrad2_kernel(WgArgs a) {
     }
   }
   const int ci = ci0 + wci * 32 + l32;
+  float* const dwp = a.dw + (int64_t)split * a.Cout * a.Cin * 9;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      atomicAdd(a.dw + ((int64_t)co * a.Cin + ci) * 9 + t, acc[t][r]);
+      dwp[((int64_t)co * a.Cin + ci) * 9 + t] = acc[t][r];
     }
-  if (a.db && cig == 0) atomicAdd(a.db + co0 + (tid & 63), bacc);
+  if (a.db && cig == 0) a.db[(int64_t)split * a.Cout + co0 + (tid & 63)] = bacc;
 #undef WG2_ITEM
 #undef WG2_HALO
 }
@@ -738,12 +741,13 @@ __global__ __launch_bounds__(256, 2) void wgrad3_kernel(WgArgs a) {
     }
   }
   const int ci = ci0 + wci * 32 + l32;
+  float* const dwp = a.dw + (int64_t)split * a.Cout * a.Cin * 9;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      atomicAdd(a.dw + ((int64_t)co * a.Cin + ci) * 9 + t, acc[t][r]);
+      dwp[((int64_t)co * a.Cin + ci) * 9 + t] = acc[t][r];
     }
   if (a.db && cig == 0) {
 #pragma unroll
@@ -752,7 +756,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3_kernel(WgArgs a) {
       v += __shfl_xor(v, 1, 64);
       v += __shfl_xor(v, 2, 64);
       v += __shfl_xor(v, 4, 64);
-      if ((tid & 7) == 0) atomicAdd(a.db + co0 + ((tid + 256 * k) >> 3), v);
+      if ((tid & 7) == 0) a.db[(int64_t)split * a.Cout + co0 + ((tid + 256 * k) >> 3)] = v;
     }
   }
 }
@@ -819,10 +823,63 @@ int ast_pad_up_adjoint_f32(const float* dp_full, float* dx, long long planes, in
   return (int)hipGetLastError();
 }
 
+}  // extern "C"
+
+namespace {
+// Launch plan shared by the wgrad entry point and its workspace query: the kernel family, its
+// tile grid and the number of pixel-range splits (each split's partial dW/db is one workspace slot).
+struct WgPlan {
+  bool small;  // wgrad_smallco_kernel
+  int tiles_x, tiles_y, groups;
+  int64_t ntiles, tiles_per_block, splits;
+};
+
+WgPlan wgrad_plan(int n, int cin, int h_in, int w_in, int cout, int upsample) {
+  WgPlan p{};
+  const int H = h_in * upsample, W = w_in * upsample;
+  p.small = (cout <= 4 || (cout <= 16 && cin <= 16)) && !g_wgrad_v1;
+  int64_t target;
+  if (p.small) {  // VALU reduction (wgrad_smallco_kernel)
+    const int cg = cout <= 4 ? 4 : 1;  // input channels per workgroup (accumulators: cout x cg x 9)
+    p.tiles_x = cdiv(W, SC_TW);
+    p.tiles_y = cdiv(H, SC_TH);
+    p.groups = cdiv(cin, cg);
+    target = 2048;
+  } else {
+    p.tiles_x = cdiv(W, WG_TW);
+    p.tiles_y = cdiv(H, WG_TH);
+    p.groups = cdiv(cout, WG_CO) * cdiv(cin, WG_CI);
+    target = 1024;  // ~1024 workgroups (4 per CU); each sweeps a contiguous range of pixel tiles
+  }
+  p.ntiles = (int64_t)p.tiles_x * p.tiles_y * n;
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(p.ntiles, (target + p.groups - 1) / p.groups));
+  p.tiles_per_block = (p.ntiles + splits - 1) / splits;
+  p.splits = (p.ntiles + p.tiles_per_block - 1) / p.tiles_per_block;
+  return p;
+}
+
+void wgrad_env() {
+  static const int v1 = [] {
+    const char* v = getenv("AST_WGRAD_V1");
+    return v ? atoi(v) : 0;
+  }();
+  g_wgrad_v1 = v1;
+}
+}  // namespace
+
+extern "C" {
+
+long long ast_conv3x3_wgrad_workspace_floats(int n, int cin, int h_in, int w_in, int cout, int upsample) {
+  if (n <= 0 || cin <= 0 || h_in <= 0 || w_in <= 0 || cout <= 0 || (upsample != 1 && upsample != 2)) return 0;
+  wgrad_env();
+  const WgPlan p = wgrad_plan(n, cin, h_in, w_in, cout, upsample);
+  return (long long)(p.splits * ((int64_t)cout * cin * 9 + cout));
+}
+
 int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* db, int n, int cin, int h_in,
                              int w_in, int cout, int upsample, int pad_mode, int dy_pitch, long long dy_plane,
-                             long long dy_offset, void* stream) {
-  if (!x || !dy || !dw) return AST_E_NULLPTR;
+                             long long dy_offset, float* workspace, long long workspace_floats, void* stream) {
+  if (!x || !dy || !dw || !workspace) return AST_E_NULLPTR;
   if (n <= 0 || cin <= 0 || h_in <= 0 || w_in <= 0 || cout <= 0) return AST_E_SHAPE;
   if (upsample != 1 && upsample != 2) return AST_E_UNSUPPORTED;
   if (pad_mode != 0 && pad_mode != 1) return AST_E_UNSUPPORTED;
@@ -834,34 +891,25 @@ int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* 
     dy_offset = 0;
   }
   if (dy_pitch < W || dy_plane < (long long)H * dy_pitch || dy_offset < 0) return AST_E_SHAPE;
+  if (workspace_floats < ast_conv3x3_wgrad_workspace_floats(n, cin, h_in, w_in, cout, upsample)) return AST_E_SHAPE;
   hipStream_t s = (hipStream_t)stream;
-  static const int v1 = [] {
-    const char* v = getenv("AST_WGRAD_V1");
-    return v ? atoi(v) : 0;
-  }();
-  g_wgrad_v1 = v1;
-  hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * (size_t)cout * cin * 9, s);
-  if (e != hipSuccess) return (int)e;
-  if (db) {
-    e = hipMemsetAsync(db, 0, sizeof(float) * (size_t)cout, s);
-    if (e != hipSuccess) return (int)e;
-  }
+  wgrad_env();
+  const WgPlan p = wgrad_plan(n, cin, h_in, w_in, cout, upsample);
+  const int64_t wcount = (int64_t)cout * cin * 9;
   WgArgs a{};
-  a.x = x; a.dy = dy; a.dw = dw; a.db = db;
+  a.x = x; a.dy = dy;
+  a.dw = workspace;                                      // [splits][cout][cin][9]
+  a.db = db ? workspace + p.splits * wcount : nullptr;  // [splits][cout]
   a.N = n; a.Cin = cin; a.Hin = h_in; a.Win = w_in; a.Cout = cout; a.reflect = pad_mode;
   a.dy_pitch = dy_pitch; a.dy_plane = dy_plane; a.dy_off = dy_offset;
-  if ((cout <= 4 || (cout <= 16 && cin <= 16)) && !g_wgrad_v1) {  // VALU reduction (wgrad_smallco_kernel)
-    const int cg = cout <= 4 ? 4 : 1;  // input channels per workgroup (accumulators: cout x cg x 9)
-    a.tiles_x = cdiv(W, SC_TW);
-    a.tiles_y = cdiv(H, SC_TH);
-    a.ntiles = (int64_t)a.tiles_x * a.tiles_y * n;
-    const int groups = cdiv(cin, cg);
-    int64_t splits = std::max<int64_t>(1, std::min<int64_t>(a.ntiles, (2048 + groups - 1) / groups));
-    a.tiles_per_block = (a.ntiles + splits - 1) / splits;
-    splits = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
-    const int64_t nb = splits * groups;
-    if (nb >= 0x7fffffff) return AST_E_SHAPE;
-    const dim3 grid((unsigned)nb);
+  a.tiles_x = p.tiles_x;
+  a.tiles_y = p.tiles_y;
+  a.ntiles = p.ntiles;
+  a.tiles_per_block = p.tiles_per_block;
+  const int64_t nblk = p.splits * p.groups;
+  if (nblk >= 0x7fffffff) return AST_E_SHAPE;
+  if (p.small) {
+    const dim3 grid((unsigned)nblk);
     if (cout <= 3) {
       if (upsample == 2) hipLaunchKernelGGL((wgrad_smallco_kernel<3, 4, 2>), grid, dim3(256), 0, s, a);
       else hipLaunchKernelGGL((wgrad_smallco_kernel<3, 4, 1>), grid, dim3(256), 0, s, a);
@@ -872,52 +920,49 @@ int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* 
       if (upsample == 2) hipLaunchKernelGGL((wgrad_smallco_kernel<16, 1, 2>), grid, dim3(256), 0, s, a);
       else hipLaunchKernelGGL((wgrad_smallco_kernel<16, 1, 1>), grid, dim3(256), 0, s, a);
     }
-    return (int)hipGetLastError();
-  }
-  a.tiles_x = cdiv(W, WG_TW);
-  a.tiles_y = cdiv(H, WG_TH);
-  a.ntiles = (int64_t)a.tiles_x * a.tiles_y * n;
-  const int groups = cdiv(cout, WG_CO) * cdiv(cin, WG_CI);
-  // ~1024 workgroups (4 per CU); each sweeps a contiguous range of pixel tiles
-  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(a.ntiles, (1024 + groups - 1) / groups));
-  a.tiles_per_block = (a.ntiles + splits - 1) / splits;
-  splits = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
-  const int64_t nblk = splits * groups;
-  if (nblk >= 0x7fffffff) return AST_E_SHAPE;
-  const bool aligned = cin % WG_CI == 0 && cout % WG_CO == 0 && W % WG_TW == 0 && H % WG_TH == 0 && w_in % 4 == 0 &&
-                       a.ntiles < 0x7fffffff && (int64_t)n * cin * h_in * w_in < 0x7fffffffLL &&
-                       (int64_t)cout * dy_plane < 0x7fffffffLL && !g_wgrad_v1;
-  static const int wver = [] {
-    const char* v = getenv("AST_WGRAD_VERSION");   // 2 = the fp32 MFMA wgrad2 kernel (A/B measurements)
-    return v ? atoi(v) : 3;
-  }();
-  if (aligned && wver >= 3) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)wgrad3_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                Wg3Cfg<1>::LDS);
-      (void)hipFuncSetAttribute((const void*)wgrad3_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                Wg3Cfg<2>::LDS);
-      attr = true;
-    }
-    if (upsample == 2)
-      hipLaunchKernelGGL(wgrad3_kernel<2>, dim3((unsigned)nblk), dim3(256), Wg3Cfg<2>::LDS, s, a);
+  } else {
+    const bool aligned = cin % WG_CI == 0 && cout % WG_CO == 0 && W % WG_TW == 0 && H % WG_TH == 0 && w_in % 4 == 0 &&
+                         a.ntiles < 0x7fffffff && (int64_t)n * cin * h_in * w_in < 0x7fffffffLL &&
+                         (int64_t)cout * dy_plane < 0x7fffffffLL && !g_wgrad_v1;
+    static const int wver = [] {
+      const char* v = getenv("AST_WGRAD_VERSION");   // 2 = the fp32 MFMA wgrad2 kernel (A/B measurements)
+      return v ? atoi(v) : 3;
+    }();
+    if (aligned && wver >= 3) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)wgrad3_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  Wg3Cfg<1>::LDS);
+        (void)hipFuncSetAttribute((const void*)wgrad3_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  Wg3Cfg<2>::LDS);
+        attr = true;
+      }
+      if (upsample == 2)
+        hipLaunchKernelGGL(wgrad3_kernel<2>, dim3((unsigned)nblk), dim3(256), Wg3Cfg<2>::LDS, s, a);
+      else
+        hipLaunchKernelGGL(wgrad3_kernel<1>, dim3((unsigned)nblk), dim3(256), Wg3Cfg<1>::LDS, s, a);
+    } else if (aligned && upsample == 2)
+      hipLaunchKernelGGL(wgrad2_kernel<2>, dim3((unsigned)nblk), dim3(256), WgCfg<2>::LDS, s, a);
+    else if (aligned)
+      hipLaunchKernelGGL(wgrad2_kernel<1>, dim3((unsigned)nblk), dim3(256), WgCfg<1>::LDS, s, a);
+    else if (upsample == 2)
+      hipLaunchKernelGGL(wgrad_kernel<2>, dim3((unsigned)nblk), dim3(256), WgCfg<2>::LDS, s, a);
     else
-      hipLaunchKernelGGL(wgrad3_kernel<1>, dim3((unsigned)nblk), dim3(256), Wg3Cfg<1>::LDS, s, a);
-  } else if (aligned && upsample == 2)
-    hipLaunchKernelGGL(wgrad2_kernel<2>, dim3((unsigned)nblk), dim3(256), WgCfg<2>::LDS, s, a);
-  else if (aligned)
-    hipLaunchKernelGGL(wgrad2_kernel<1>, dim3((unsigned)nblk), dim3(256), WgCfg<1>::LDS, s, a);
-  else if (upsample == 2)
-    hipLaunchKernelGGL(wgrad_kernel<2>, dim3((unsigned)nblk), dim3(256), WgCfg<2>::LDS, s, a);
-  else
-    hipLaunchKernelGGL(wgrad_kernel<1>, dim3((unsigned)nblk), dim3(256), WgCfg<1>::LDS, s, a);
-  return (int)hipGetLastError();
+      hipLaunchKernelGGL(wgrad_kernel<1>, dim3((unsigned)nblk), dim3(256), WgCfg<1>::LDS, s, a);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  // the splits' partials, summed in split order
+  e = ast_det::reduce_cols(workspace, p.splits, wcount, wcount, 1, 0, dw, 0, false, s);
+  if (e == hipSuccess && db) e = ast_det::reduce_cols(a.db, p.splits, cout, cout, 1, 0, db, 0, false, s);
+  return (int)e;
 }
 
 int ast_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, float* db, int n, int cin, int h_in, int w_in,
-                          int cout, int upsample, int pad_mode, void* stream) {
-  return ast_conv3x3_wgrad_ex_f32(x, dy, dw, db, n, cin, h_in, w_in, cout, upsample, pad_mode, 0, 0, 0, stream);
+                          int cout, int upsample, int pad_mode, float* workspace, long long workspace_floats,
+                          void* stream) {
+  return ast_conv3x3_wgrad_ex_f32(x, dy, dw, db, n, cin, h_in, w_in, cout, upsample, pad_mode, 0, 0, 0, workspace,
+                                  workspace_floats, stream);
 }
 
 }  // extern "C"

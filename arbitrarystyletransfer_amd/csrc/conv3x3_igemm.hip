@@ -1242,7 +1242,9 @@ int auto_config(int cin, int cout, int n, int h, int w, int up, bool pool, bool 
 
 extern "C" {
 
-const char* ast_version(void) { return "ast_hip 0.1 gfx950"; }
+const char* ast_version(void) { return "ast_hip 0.3 gfx950"; }
+
+int ast_loss_acc_floats(void) { return AST_LOSS_ACC_FLOATS; }
 
 size_t ast_conv3x3_packed_numel(int cout, int cin) {
   if (cout <= 0 || cin <= 0) return 0;

@@ -10,13 +10,17 @@
 // i.e. phi_k = S_k - S_{k+1}, S_j = sig((x - jL)/W): 257 sigmoids per value would give all bins,
 // but with L/W = 2.5 a bin d bins away from x gets < e^{-2.5(d-1)}; the kernel evaluates the
 // window |j - x/L| <= kHalo (kHalo = 12: the neglected mass is < e^{-27} ~ 2e-12 of each value's
-// unit mass, far below fp32 resolution of a bin). Per workgroup an LDS histogram (ds_add_f32),
-// flushed with one global atomic per bin. HBM-bound (one read of x); the window's sigmoids run on
-// the transcendental unit.
+// unit mass, far below fp32 resolution of a bin). The bins are accumulated as exact 32.32
+// fixed-point integers (each contribution phi in [0, 1] truncated to a multiple of 2^-32): integer
+// addition is associative, so the per-workgroup LDS histograms (ds_add_u64) and their flush into
+// the per-image workspace histogram (one 64-bit atomic per bin) give the same bits in any order.
+// A NaN anywhere in an image poisons all its bins (a flag), as the reference's dense sum does.
+// HBM-bound (one read of x); the window's sigmoids run on the transcendental unit.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
 #include "../../include/ast_hip.h"
+#include "det.h"
 
 namespace {
 
@@ -50,17 +54,21 @@ __device__ __forceinline__ void window(float x, int& j0, int& j1) {
   j1 = min(kBins, (int)ceilf(hi));
 }
 
-// grid (blocks_per_image, n)
-__global__ __launch_bounds__(kThreads) void soft_hist_kernel(const float* __restrict__ x, int64_t m, float inv_norm,
-                                                             float* __restrict__ hist) {
-  __shared__ float hs[kBins];
-  for (int i = threadIdx.x; i < kBins; i += kThreads) hs[i] = 0.f;
+// grid (blocks_per_image, n); acc [n][kBins + 1] int64 (the bins, then the NaN flag), zeroed
+constexpr double kFix = 4294967296.0;  // 2^32
+
+__global__ __launch_bounds__(kThreads) void soft_hist_kernel(const float* __restrict__ x, int64_t m,
+                                                             unsigned long long* __restrict__ acc) {
+  __shared__ unsigned long long hs[kBins];
+  __shared__ int nan_seen;
+  for (int i = threadIdx.x; i < kBins; i += kThreads) hs[i] = 0ull;
+  if (threadIdx.x == 0) nan_seen = 0;
   __syncthreads();
   const float* xb = x + (int64_t)blockIdx.y * m;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < m; i += (int64_t)gridDim.x * kThreads) {
     const float v = xb[i];
     if (!(v == v)) {  // NaN poisons every bin, as in the reference's dense sum
-      for (int k = 0; k < kBins; ++k) atomicAdd(&hs[k], v);
+      nan_seen = 1;
       continue;
     }
     int j0, j1;
@@ -69,17 +77,30 @@ __global__ __launch_bounds__(kThreads) void soft_hist_kernel(const float* __rest
     float sprev = sigm((v - (float)j0 * kL) * kInvW);
     for (int j = j0 + 1; j <= j1; ++j) {
       const float s = sigm((v - (float)j * kL) * kInvW);
-      atomicAdd(&hs[j - 1], sprev - s);  // bin j-1 = S_{j-1} - S_j
+      // bin j-1 = S_{j-1} - S_j >= 0 (S decreases in j); x 2^32 is exact in fp32, the conversion
+      // truncates the sub-2^-32 tail
+      atomicAdd(&hs[j - 1], (unsigned long long)(fmaxf(sprev - s, 0.f) * 4294967296.0f));
       sprev = s;
     }
   }
   __syncthreads();
-  float* hb = hist + (int64_t)blockIdx.y * kBins;
-  for (int i = threadIdx.x; i < kBins; i += kThreads) atomicAdd(&hb[i], hs[i] * inv_norm);
+  unsigned long long* hb = acc + (int64_t)blockIdx.y * (kBins + 1);
+  for (int i = threadIdx.x; i < kBins; i += kThreads)
+    if (hs[i]) atomicAdd(&hb[i], hs[i]);
+  if (threadIdx.x == 0 && nan_seen) atomicOr(&hb[kBins], 1ull);
 }
 
-__global__ void zero_kernel(float* p, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0.f;
+__global__ void hist_finish_kernel(const unsigned long long* __restrict__ acc, int n, float inv_norm,
+                                   float* __restrict__ hist) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * kBins) return;
+  const int b = e / kBins, k = e - b * kBins;
+  const unsigned long long* hb = acc + (int64_t)b * (kBins + 1);
+  hist[e] = hb[kBins] ? __builtin_nanf("") : (float)((double)hb[k] * (1.0 / kFix) * (double)inv_norm);
+}
+
+__global__ void zero_u64_kernel(unsigned long long* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0ull;
 }
 
 // EMD of the two histograms' CDFs (losses.py:8-22), one workgroup per image:
@@ -106,7 +127,7 @@ __global__ __launch_bounds__(kBins) void emd_kernel(const float* __restrict__ hx
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if ((t & 63) == 0) sh[t >> 6] = s;
   __syncthreads();
-  if (t == 0 && loss) atomicAdd(loss, w_over_n * ((sh[0] + sh[1]) + (sh[2] + sh[3])));
+  if (loss) ast_det::loss_acc_commit(loss, w_over_n * ((sh[0] + sh[1]) + (sh[2] + sh[3])));
   if (!ghist) return;
   // suffix sum of e: sum_{u >= t} e_u
   __syncthreads();
@@ -173,7 +194,7 @@ __global__ void range_loss_kernel(const float* __restrict__ x, int64_t n, float 
     }
   }
   const float t = block_sum(s, sh);
-  if (threadIdx.x == 0 && loss) atomicAdd(loss, w_over_n * t);
+  if (loss) ast_det::loss_acc_commit(loss, w_over_n * t);
 }
 
 // w * mean((x - y)^2); dx = 2 w (x - y) / n
@@ -191,32 +212,39 @@ __global__ void sqdiff_kernel(const float* __restrict__ x, const float* __restri
     }
   }
   const float t = block_sum(s, sh);
-  if (threadIdx.x == 0 && loss) atomicAdd(loss, w_over_n * t);
+  if (loss) ast_det::loss_acc_commit(loss, w_over_n * t);
 }
 
 unsigned grid_for(int64_t n, int64_t per_block_min) {
   int64_t b = (n + per_block_min - 1) / per_block_min;
-  return (unsigned)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
+  return (unsigned)(b < 1 ? 1 : (b > AST_LOSS_SLOTS ? AST_LOSS_SLOTS : b));
 }
 
 }  // namespace
 
 extern "C" {
 
-int ast_soft_hist_f32(const float* x, int n, long long m, float inv_norm, float* hist, void* stream) {
-  if (!x || !hist) return AST_E_NULLPTR;
-  if (n <= 0 || m <= 0 || n > 65535) return AST_E_SHAPE;
+long long ast_soft_hist_workspace_floats(int n) { return n > 0 ? 2LL * n * (kBins + 1) : 0; }
+
+int ast_soft_hist_f32(const float* x, int n, long long m, float inv_norm, float* hist, float* workspace,
+                      long long workspace_floats, void* stream) {
+  if (!x || !hist || !workspace) return AST_E_NULLPTR;
+  if (n <= 0 || m <= 0 || n > 65535 || m >= (1LL << 30)) return AST_E_SHAPE;
+  if (workspace_floats < ast_soft_hist_workspace_floats(n) || ((uintptr_t)workspace & 7)) return AST_E_SHAPE;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(kThreads), 0, st, hist, (int64_t)n * kBins);
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(workspace);
+  hipLaunchKernelGGL(zero_u64_kernel, dim3(1), dim3(kThreads), 0, st, acc, (int64_t)n * (kBins + 1));
   const unsigned bpi = grid_for(m, 8 * kThreads) > 512 ? 512 : grid_for(m, 8 * kThreads);
-  hipLaunchKernelGGL(soft_hist_kernel, dim3(bpi, n), dim3(kThreads), 0, st, x, (int64_t)m, inv_norm, hist);
+  hipLaunchKernelGGL(soft_hist_kernel, dim3(bpi, n), dim3(kThreads), 0, st, x, (int64_t)m, acc);
+  hipLaunchKernelGGL(hist_finish_kernel, dim3((n * kBins + kThreads - 1) / kThreads), dim3(kThreads), 0, st, acc, n,
+                     inv_norm, hist);
   return (int)hipGetLastError();
 }
 
 int ast_emd_loss_f32(const float* hx, const float* hy, int n, float weight, const float* gscale, float* loss,
                      float* ghist, void* stream) {
   if (!hx || !hy || (!loss && !ghist)) return AST_E_NULLPTR;
-  if (n <= 0) return AST_E_SHAPE;
+  if (n <= 0 || n > AST_LOSS_SLOTS) return AST_E_SHAPE;
   hipLaunchKernelGGL(emd_kernel, dim3(n), dim3(kBins), 0, (hipStream_t)stream, hx, hy, weight / (float)n, gscale,
                      loss, ghist);
   return (int)hipGetLastError();

@@ -1,17 +1,19 @@
 // Style-transfer losses for gfx950: losses.py gram_matrix (105-109), compute_content_loss
 // (124-126), compute_style_loss (128-139), tv_loss (90-103), with mean_variance_norm
-// (models.py:64-68) fused into the content term. Each loss kernel produces its value (atomically
-// added into a device scalar) and, when asked, the input gradient, so the training step needs no
-// separate backward pass through PyTorch.
+// (models.py:64-68) fused into the content term. Each loss kernel produces its value (added into a
+// loss accumulator, det.h: per-workgroup partials summed in a fixed order) and, when asked, the
+// input gradient, so the training step needs no separate backward pass through PyTorch.
 //
-//  * gram: batched fp32 MFMA GEMM G[b] = s·F[b]F[b]^T (F = C x HW), split-K over HW with fp32
-//    atomics into G (C <= 512, HW up to 512^2: few output tiles, very long K).
+//  * gram: batched fp32 MFMA GEMM G[b] = s·F[b]F[b]^T (F = C x HW), split-K over HW (C <= 512, HW
+//    up to 512^2: few output tiles, very long K); the splits' partial tiles are summed in split
+//    order (det.h), never through atomics.
 //  * gram backward: dF[b] (+)= s·(dG+dG^T)[b]·F[b] + ra[b,i]·F[b][i,:] + rb[b,i] — the GEMM
 //    epilogue also adds the mean/std-term gradients of compute_style_loss (per-plane affine in F).
 //  * Huber: delta = 1, reduction 'mean' (F.huber_loss default).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/ast_hip.h"
+#include "det.h"
 
 namespace {
 
@@ -123,34 +125,37 @@ __device__ void plane_mean_std2(const float* __restrict__ p, const float* __rest
 // Forward: one read of x and y for both planes' moments, one for the Huber sums. With pstats,
 // also keeps per plane (mu_x, sd_x, mu_y, sd_y, mean(g), sum(g z)/(N-1)) for the backward.
 __global__ __launch_bounds__(kThreads) void mvn_huber_kernel(const float* __restrict__ x, const float* __restrict__ y,
-                                                             int64_t hw, float inv_numel, float w, float* loss,
-                                                             float* __restrict__ pstats) {
+                                                             int64_t planes, int64_t hw, float inv_numel, float w,
+                                                             float* loss, float* __restrict__ pstats) {
   __shared__ float sh[12];
-  const int64_t p = blockIdx.x;
-  const float* xp = x + p * hw;
-  const float* yp = y + p * hw;
-  float mx, sx, my, sy;
-  plane_mean_std2(xp, yp, hw, 1e-5f, sh, mx, sx, my, sy);
-  float sh_ = 0.f, sg = 0.f, sgz = 0.f;
-  for (int64_t i = threadIdx.x; i < hw; i += kThreads) {
-    const float z = (xp[i] - mx) / sx;
-    const float d = z - (yp[i] - my) / sy;
-    sh_ += huber(d);
-    const float g = huber_grad(d);
-    sg += g;
-    sgz += g * z;
+  float Hs = 0.f;  // this workgroup's planes, in plane order
+  for (int64_t p = blockIdx.x; p < planes; p += gridDim.x) {
+    const float* xp = x + p * hw;
+    const float* yp = y + p * hw;
+    float mx, sx, my, sy;
+    plane_mean_std2(xp, yp, hw, 1e-5f, sh, mx, sx, my, sy);
+    float sh_ = 0.f, sg = 0.f, sgz = 0.f;
+    for (int64_t i = threadIdx.x; i < hw; i += kThreads) {
+      const float z = (xp[i] - mx) / sx;
+      const float d = z - (yp[i] - my) / sy;
+      sh_ += huber(d);
+      const float g = huber_grad(d);
+      sg += g;
+      sgz += g * z;
+    }
+    Hs += block_sum(sh_, sh);
+    if (pstats) {
+      const float G = block_sum(sg, sh);
+      const float GZ = block_sum(sgz, sh);
+      if (threadIdx.x == 0) {
+        float* s = pstats + 6 * p;
+        s[0] = mx; s[1] = sx; s[2] = my; s[3] = sy;
+        s[4] = G / (float)hw;
+        s[5] = GZ / (float)(hw - 1);
+      }
+    }
   }
-  const float H = block_sum(sh_, sh);
-  if (threadIdx.x == 0 && loss) atomicAdd(loss, w * H * inv_numel);
-  if (!pstats) return;
-  const float G = block_sum(sg, sh);
-  const float GZ = block_sum(sgz, sh);
-  if (threadIdx.x == 0) {
-    float* s = pstats + 6 * p;
-    s[0] = mx; s[1] = sx; s[2] = my; s[3] = sy;
-    s[4] = G / (float)hw;
-    s[5] = GZ / (float)(hw - 1);
-  }
+  if (loss) ast_det::loss_acc_commit(loss, w * Hs * inv_numel);
 }
 
 // Backward: dx = c * (huber'(d) - mean(g) - z * sum(g z)/(N-1)) / sd_x, one read of x and y.
@@ -218,7 +223,7 @@ __global__ void huber_kernel(const float* __restrict__ x, const float* __restric
     }
   }
   const float t = block_sum(s, sh);
-  if (threadIdx.x == 0 && loss) atomicAdd(loss, w * t * inv_numel);
+  if (loss) ast_det::loss_acc_commit(loss, w * t * inv_numel);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -258,7 +263,7 @@ __global__ void style_moment_loss_kernel(const float* __restrict__ stats, int64_
     }
   }
   const float t = block_sum(s, sh);
-  if (threadIdx.x == 0 && loss) atomicAdd(loss, w * 1.25f * t * inv);
+  if (loss) ast_det::loss_acc_commit(loss, w * 1.25f * t * inv);
 }
 
 // Gram huber: loss += w*10*mean(huber(Gx-Gy)); dG = w*10*huber'(Gx-Gy)/numel (gscale'd).
@@ -274,7 +279,7 @@ __global__ void gram_huber_kernel(const float* __restrict__ gx, const float* __r
     if (dg) dg[i] = c * huber_grad(d);
   }
   const float t = block_sum(s, sh);
-  if (threadIdx.x == 0 && loss) atomicAdd(loss, w * 10.f * t * inv);
+  if (loss) ast_det::loss_acc_commit(loss, w * 10.f * t * inv);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -306,11 +311,12 @@ __global__ void tv_kernel(const float* __restrict__ x, int64_t planes, int H, in
     if (dx) dx[i] = accumulate ? dx[i] + c * g : c * g;
   }
   const float t = block_sum(s, sh);
-  if (threadIdx.x == 0 && loss) atomicAdd(loss, w * t);
+  if (loss) ast_det::loss_acc_commit(loss, w * t);
 }
 
 // ------------------------------------------------------------------------------------------
-// Gram forward: G[b][i][j] += s * sum_k F[b][i][k] F[b][j][k], k-range split over blockIdx.y.
+// Gram forward: G[blockIdx.y][b][i][j] = s * sum_{k in split} F[b][i][k] F[b][j][k], k-range split over
+// blockIdx.y (G is the gram itself with one split, else the workspace of partial tiles).
 // 64x64 output tile, 4 waves (2x2 of 32x32), BK = 32; F tiles transposed into LDS [k][row].
 // ------------------------------------------------------------------------------------------
 constexpr int GT = 64, GBK = 32;
@@ -366,12 +372,12 @@ __global__ __launch_bounds__(256) void gram_kernel(const float* __restrict__ F, 
     }
     __syncthreads();
   }
-  float* Gb = G + (int64_t)b * C * C;
+  float* Gb = G + ((int64_t)blockIdx.y * gridDim.z + b) * C * C;
   const int j = tj * GT + wj * 32 + l32;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int i = ti * GT + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (i < C && j < C) atomicAdd(Gb + (int64_t)i * C + j, s * acc[r]);
+    if (i < C && j < C) Gb[(int64_t)i * C + j] = s * acc[r];
   }
 }
 
@@ -459,27 +465,55 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
   }
 }
 
-int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, 4096)); }
+int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, AST_LOSS_SLOTS)); }
 
 }  // namespace
 
 extern "C" {
 
-int ast_gram_f32(const float* feat, float* gram, int n, int c, long long hw, float scale, void* stream) {
-  if (!feat || !gram) return AST_E_NULLPTR;
-  if (n <= 0 || c <= 0 || hw <= 0 || n > 65535) return AST_E_SHAPE;
-  hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemsetAsync(gram, 0, sizeof(float) * (size_t)n * c * c, s);
-  if (e != hipSuccess) return (int)e;
+}  // extern "C"
+
+namespace {
+// split-K plan of the gram launch: >= ~1024 workgroups, chunks a multiple of GBK
+int64_t gram_splits(int n, int c, int64_t hw, int64_t* kchunk_out) {
   const int tiles = (c + GT - 1) / GT;
-  // split K so that the launch has >= ~1024 workgroups, chunks a multiple of GBK
   int64_t splits = std::max<int64_t>(1, std::min<int64_t>((hw + 1023) / 1024, 1024 / std::max(1, n * tiles * tiles) + 1));
   int64_t kchunk = (hw + splits - 1) / splits;
   kchunk = (kchunk + GBK - 1) / GBK * GBK;
   splits = (hw + kchunk - 1) / kchunk;
+  if (kchunk_out) *kchunk_out = kchunk;
+  return splits;
+}
+}  // namespace
+
+extern "C" {
+
+long long ast_gram_workspace_floats(int n, int c, long long hw) {
+  if (n <= 0 || c <= 0 || hw <= 0) return 0;
+  const int64_t splits = gram_splits(n, c, hw, nullptr);
+  return splits > 1 ? (long long)(splits * n * c * c) : 0;
+}
+
+int ast_gram_f32(const float* feat, float* gram, int n, int c, long long hw, float scale, float* workspace,
+                 long long workspace_floats, void* stream) {
+  if (!feat || !gram) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hw <= 0 || n > 65535) return AST_E_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  const int tiles = (c + GT - 1) / GT;
+  int64_t kchunk = 0;
+  const int64_t splits = gram_splits(n, c, hw, &kchunk);
   if (splits > 65535) return AST_E_SHAPE;
-  hipLaunchKernelGGL(gram_kernel, dim3(tiles * tiles, (unsigned)splits, n), dim3(256), 0, s, feat, gram, c,
-                     (int64_t)hw, kchunk, scale);
+  if (splits > 1) {
+    if (!workspace) return AST_E_NULLPTR;
+    if (workspace_floats < ast_gram_workspace_floats(n, c, hw)) return AST_E_SHAPE;
+  }
+  hipLaunchKernelGGL(gram_kernel, dim3(tiles * tiles, (unsigned)splits, n), dim3(256), 0, s, feat,
+                     splits > 1 ? workspace : gram, c, (int64_t)hw, kchunk, scale);
+  if (splits > 1) {
+    const int64_t cnt = (int64_t)n * c * c;
+    const hipError_t e = ast_det::reduce_cols(workspace, splits, cnt, cnt, 1, 0, gram, 0, false, s);
+    if (e != hipSuccess) return (int)e;
+  }
   return (int)hipGetLastError();
 }
 
@@ -500,7 +534,8 @@ int ast_mvn_huber_f32(const float* x, const float* y, long long planes, long lon
                       float* pstats, void* stream) {
   if (!x || !y) return AST_E_NULLPTR;
   if (planes <= 0 || hw <= 1 || planes > 0x7fffffffLL) return AST_E_SHAPE;
-  hipLaunchKernelGGL(mvn_huber_kernel, dim3((unsigned)planes), dim3(kThreads), 0, (hipStream_t)stream, x, y,
+  const unsigned grid = (unsigned)std::min<long long>(planes, AST_LOSS_SLOTS);
+  hipLaunchKernelGGL(mvn_huber_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, x, y, (int64_t)planes,
                      (int64_t)hw, (float)(1.0 / ((double)planes * hw)), weight, loss, pstats);
   return (int)hipGetLastError();
 }

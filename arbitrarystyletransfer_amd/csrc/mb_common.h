@@ -20,9 +20,22 @@ struct EdArgs {
   const float* wdw;  // depthwise weights [hid][k*k] (BN folded)
   const float* bdw;  // [hid]
   void* d;           // [n][hid][ho][wo]
-  float* pool;       // [n][hid], accumulated
+  float* pool;       // SE-pool partial sums [n][hid][slots]: one slot per output tile of an image,
+                     // plain stores (the host sums the slots in order: deterministic)
   int tiles_x, tiles_y;
+  int slots;         // output tiles per image (set by the launcher)
+  long long* plan;   // non-null: the launcher only stores its slot count here and launches nothing
 };
+
+// The launchers' plan-mode exit: the slot count of the launch that would run.
+inline bool ed_plan(EdArgs& a, long long slots) {
+  a.slots = (int)slots;
+  if (a.plan) {
+    *a.plan = slots;
+    return true;
+  }
+  return false;
+}
 
 // v4 (bf16, no upsample, expand blocks with c1 == cin, k in {3, 5}; stride 1 with cin_pad in
 // {16..96, 128}, stride 2 with cin_pad <= 64 and even wo): returns AST_E_UNSUPPORTED when the shape

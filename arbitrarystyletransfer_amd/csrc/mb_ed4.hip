@@ -285,7 +285,8 @@ __global__ __launch_bounds__(WG4 ? 64 * ED4_WGN : 64, (K == 5 && KS >= 6) ? 1 : 
     }
   }
   psum += __shfl_xor(psum, 32, 64);
-  if (h == 0 && chv) atomicAdd(a.pool + (int64_t)n * a.hid + ch, psum);
+  // one slot per (band, strip) of the image; strips past the right border (WG4 padding waves) store 0
+  if (h == 0 && chv) a.pool[((int64_t)n * a.hid + ch) * a.slots + band * (a.slots / bands) + s] = psum;
 }
 
 
@@ -300,8 +301,11 @@ int launch_ks(EdArgs a, hipStream_t st) {
   // lose 10-50% to the per-row workgroup barrier (their rows are longer and less uniform)
   if (ED4_WG4 && K == 3 && a.wo % 8 == 0) {  // WG4: 4 strips per workgroup, 16-byte D stores
     const int64_t total4 = (int64_t)ncb * ((strips + ED4_WGN - 1) / ED4_WGN) * bands * a.n, grid4 = (total4 + 7) / 8 * 8;
+    if (ed_plan(a, (int64_t)bands * ((strips + ED4_WGN - 1) / ED4_WGN) * ED4_WGN)) return 0;
     hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true, true, R1, UP>), dim3((unsigned)grid4), dim3(64 * ED4_WGN), 0, st, a,
                        strips, bands, ncb, (int)total4);
+  } else if (ed_plan(a, (int64_t)bands * strips)) {
+    return 0;
   } else if (a.wo % 4 == 0) {
     // VEC: wo % 4 == 0, so a 4-column D piece is 8-byte aligned and wholly inside or outside the row
     hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true, false, R1, UP>), dim3((unsigned)grid), dim3(64), 0, st, a,
@@ -471,7 +475,7 @@ __global__ __launch_bounds__(64, 2) void expand_dw4s2_kernel(EdArgs a, int strip
     }
   }
   psum += __shfl_xor(psum, 32, 64);
-  if (h == 0 && chv) atomicAdd(a.pool + (int64_t)n * a.hid + ch, psum);
+  if (h == 0 && chv) a.pool[((int64_t)n * a.hid + ch) * a.slots + band * strips + s] = psum;
 }
 
 template <int K, int KS>
@@ -481,6 +485,7 @@ int launch_s2_ks(EdArgs a, hipStream_t st) {
   const int64_t total = (int64_t)ncb * strips * bands * a.n;
   if (total > 0x7ffffff0LL) return AST_E_SHAPE;
   const int64_t grid = (total + 7) / 8 * 8;
+  if (ed_plan(a, (int64_t)bands * strips)) return 0;
   hipLaunchKernelGGL((expand_dw4s2_kernel<K, KS, TH>), dim3((unsigned)grid), dim3(64), 0, st, a, strips, bands, ncb,
                      (int)total);
   return (int)hipGetLastError();

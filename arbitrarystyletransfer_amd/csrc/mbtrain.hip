@@ -14,6 +14,7 @@
 #include <math.h>
 #include <stdint.h>
 #include "../../include/ast_hip.h"
+#include "det.h"
 
 namespace {
 
@@ -41,7 +42,8 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
 // GEMM: C[b][m][n] (+)= sum_k A[b][m][k] * B[b][k][n], general strides. 64x64 tile per workgroup,
 // 4 waves x 32x32 (v_mfma_f32_32x32x2_f32), K in chunks of 32 through LDS; the next chunk's global
 // loads are issued before the current chunk's MFMAs (register prefetch). grid.z = batch * ksplit;
-// with atomic != 0 partial sums are atomically added (C zeroed by the caller).
+// with part != null every (image, K-split) tile is stored dense into part[z][m][n] (z = blockIdx.z)
+// and gemm_reduce_kernel sums them in z order into C (no atomics: deterministic).
 // Folding (NCHW 1x1 convs): foldN = P folds the image index into N (column n -> image n / P, pixel
 // n % P through the batch strides of B and C), so small planes still fill 64-wide tiles; foldK = P
 // folds it into K (the weight gradient's reduction over images x pixels). Both need batch == 1.
@@ -50,8 +52,9 @@ struct GemmArgs {
   const float* A;
   const float* B;
   float* C;
+  float* part;  // partial tiles [batch * ksplit][M][N], or null: C written directly
   int64_t sAb, sAm, sAk, sBb, sBk, sBn, sCb, sCm, sCn;
-  int M, N, K, batch, ksplit, kchunk, accumulate, atomic, foldK, foldN;
+  int M, N, K, batch, ksplit, kchunk, accumulate, foldK, foldN;
 };
 
 typedef float f32x8 __attribute__((ext_vector_type(8)));
@@ -145,6 +148,15 @@ __global__ __launch_bounds__(kT) void gemm_kernel(GemmArgs a) {
   }
   const int n = n0 + wn * 32 + r;
   if (n >= a.N) return;
+  if (a.part) {
+    float* P = a.part + (int64_t)blockIdx.z * a.M * a.N + n;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (m < a.M) P[(int64_t)m * a.N] = acc[i];
+    }
+    return;
+  }
   int64_t ccol;
   if (a.foldN) {
     const int bb = n / a.foldN;
@@ -158,9 +170,39 @@ __global__ __launch_bounds__(kT) void gemm_kernel(GemmArgs a) {
     const int m = m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
     if (m < a.M) {
       float* c = C + m * a.sCm;
-      if (a.atomic) atomicAdd(c, acc[i]);
-      else *c = a.accumulate ? *c + acc[i] : acc[i];
+      *c = a.accumulate ? *c + acc[i] : acc[i];
     }
+  }
+}
+
+// C[b][m][n] (+)= sum over the tiles z of C's image (z = b * ksplit + ks; all z when C is shared
+// across the batch, sCb == 0) of part[z][m][n], in z order.
+__global__ __launch_bounds__(kT) void gemm_reduce_kernel(GemmArgs a, int zper) {
+  const int64_t mn = (int64_t)a.M * a.N;
+  const int cb = blockIdx.y;  // C image (0 when shared)
+  for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < mn; e += (int64_t)gridDim.x * kT) {
+    const float* p = a.part + (int64_t)cb * zper * mn + e;
+    float s = 0.f;
+    int z = 0;
+    for (; z + 4 <= zper; z += 4) {
+      const float v0 = p[(int64_t)z * mn], v1 = p[(int64_t)(z + 1) * mn];
+      const float v2 = p[(int64_t)(z + 2) * mn], v3 = p[(int64_t)(z + 3) * mn];
+      s += v0;
+      s += v1;
+      s += v2;
+      s += v3;
+    }
+    for (; z < zper; ++z) s += p[(int64_t)z * mn];
+    const int m = (int)(e / a.N), n = (int)(e - (int64_t)m * a.N);
+    int64_t ccol;
+    if (a.foldN) {
+      const int bb = n / a.foldN;
+      ccol = bb * a.sCb + (int64_t)(n - bb * a.foldN) * a.sCn;
+    } else {
+      ccol = (int64_t)cb * a.sCb + (int64_t)n * a.sCn;
+    }
+    float* c = a.C + ccol + (int64_t)m * a.sCm;
+    *c = a.accumulate ? *c + s : s;
   }
 }
 
@@ -278,14 +320,14 @@ __global__ __launch_bounds__(kT) void dw_fold_kernel(const float* __restrict__ d
   }
 }
 
-// dw[c][tap] += sum over a segment of one image's output plane (grid = (segments, n, c)); dw is
-// zeroed by the caller. The K*K partial sums are reduced across the wave by shuffles, across the
-// 4 waves through LDS.
+// part[c][n * segments + seg][tap] = sum over a segment of one image's output plane (grid =
+// (segments, n, c)); the K*K partial sums are reduced across the wave by shuffles, across the 4
+// waves through LDS; the host then sums each channel's (image, segment) rows in order.
 constexpr int DW_SEG = 8 * kT;
 
 template <int K, int S>
 __global__ __launch_bounds__(kT) void dw_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ g,
-                                                      float* __restrict__ dw, int c, int h, int wd, int ho, int wo) {
+                                                      float* __restrict__ part, int c, int h, int wd, int ho, int wo) {
   constexpr int P = (K - 1) / 2, KK = K * K;
   __shared__ float sh[4][KK];
   const int ch = blockIdx.z, n = blockIdx.y;
@@ -325,7 +367,8 @@ __global__ __launch_bounds__(kT) void dw_wgrad_kernel(const float* __restrict__ 
   __syncthreads();
   if (threadIdx.x < KK) {
     const int t = threadIdx.x;
-    atomicAdd(dw + (int64_t)ch * KK + t, (sh[0][t] + sh[1][t]) + (sh[2][t] + sh[3][t]));
+    const int64_t row = ((int64_t)ch * gridDim.y + n) * gridDim.x + blockIdx.x;
+    part[row * KK + t] = (sh[0][t] + sh[1][t]) + (sh[2][t] + sh[3][t]);
   }
 }
 
@@ -608,50 +651,77 @@ __global__ __launch_bounds__(kT) void se_fc_fwd_kernel(const float* __restrict__
   }
 }
 
-// SE MLP backward per image: dz = dgate * (0 < z < 1); dW2, db2, dh = W2^T dz * (hid > 0), dW1, db1,
-// dpool = W1^T dh (scaled by 1/hw for the broadcast back onto the plane). Parameter gradients are
-// accumulated with atomics (zeroed by the caller).
+// SE MLP backward, per image (one workgroup): dz = dgate * (0 < z < 1), dh = W2^T dz * (hid > 0),
+// dpool = W1^T dh (scaled by 1/hw for the broadcast back onto the plane); dz and dh go to the
+// workspace ([n][c] then [n][red]) for se_fc_param_grad_kernel.
 __global__ __launch_bounds__(kT) void se_fc_bwd_kernel(const float* __restrict__ dgate, const float* __restrict__ z,
-                                                       const float* __restrict__ hid, const float* __restrict__ pool,
-                                                       const float* __restrict__ w1, const float* __restrict__ w2,
-                                                       int c, int red, float inv_hw, float* __restrict__ dw1,
-                                                       float* __restrict__ db1, float* __restrict__ dw2,
-                                                       float* __restrict__ db2, float* __restrict__ dpool) {
+                                                       const float* __restrict__ hid, const float* __restrict__ w1,
+                                                       const float* __restrict__ w2, int n_img, int c, int red,
+                                                       float inv_hw, float* __restrict__ ws,
+                                                       float* __restrict__ dpool) {
   extern __shared__ float sm[];
   float* dz = sm;        // [c]
   float* dh = sm + c;    // [red]
   const int n = blockIdx.x;
+  float* dzg = ws + (int64_t)n * c;
+  float* dhg = ws + (int64_t)n_img * c + (int64_t)n * red;
   for (int i = threadIdx.x; i < c; i += kT) {
     const float zv = z[(int64_t)n * c + i];
     const float d = (zv > 0.f && zv < 1.f) ? dgate[(int64_t)n * c + i] : 0.f;
     dz[i] = d;
-    atomicAdd(db2 + i, d);
+    dzg[i] = d;
   }
   __syncthreads();
   const float* hv = hid + (int64_t)n * red;
-  for (int e = threadIdx.x; e < c * red; e += kT) {
-    const int i = e / red, j = e % red;
-    atomicAdd(dw2 + e, dz[i] * hv[j]);
-  }
   for (int j = threadIdx.x; j < red; j += kT) {
     float a = 0.f;
 #pragma unroll 16
     for (int i = 0; i < c; ++i) a = fmaf(w2[(int64_t)i * red + j], dz[i], a);
     a = hv[j] > 0.f ? a : 0.f;
     dh[j] = a;
-    atomicAdd(db1 + j, a);
+    dhg[j] = a;
   }
   __syncthreads();
-  const float* pv = pool + (int64_t)n * c;
-  for (int e = threadIdx.x; e < red * c; e += kT) {
-    const int j = e / c, i = e % c;
-    atomicAdd(dw1 + e, dh[j] * pv[i]);
-  }
   for (int i = threadIdx.x; i < c; i += kT) {
     float a = 0.f;
 #pragma unroll 16
     for (int j = 0; j < red; ++j) a = fmaf(w1[(int64_t)j * c + i], dh[j], a);
     dpool[(int64_t)n * c + i] = a * inv_hw;
+  }
+}
+
+// SE parameter gradients, one thread per parameter, summed over the images in image order:
+// dW2[i][j] = sum_n dz[n][i] hid[n][j], db2[i] = sum_n dz[n][i], dW1[j][i] = sum_n dh[n][j] pool[n][i],
+// db1[j] = sum_n dh[n][j].
+__global__ __launch_bounds__(kT) void se_fc_param_grad_kernel(const float* __restrict__ ws,
+                                                              const float* __restrict__ hid,
+                                                              const float* __restrict__ pool, int n_img, int c,
+                                                              int red, float* __restrict__ dw1,
+                                                              float* __restrict__ db1, float* __restrict__ dw2,
+                                                              float* __restrict__ db2) {
+  const float* dz = ws;
+  const float* dh = ws + (int64_t)n_img * c;
+  const int64_t cr = (int64_t)c * red, total = 2 * cr + c + red;
+  for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
+    float s = 0.f;
+    if (e < cr) {  // dW2[i][j]
+      const int i = (int)(e / red), j = (int)(e - (int64_t)i * red);
+      for (int n = 0; n < n_img; ++n) s = fmaf(dz[(int64_t)n * c + i], hid[(int64_t)n * red + j], s);
+      dw2[e] = s;
+    } else if (e < 2 * cr) {  // dW1[j][i]
+      const int64_t f = e - cr;
+      const int j = (int)(f / c), i = (int)(f - (int64_t)j * c);
+      for (int n = 0; n < n_img; ++n) s = fmaf(dh[(int64_t)n * red + j], pool[(int64_t)n * c + i], s);
+      dw1[f] = s;
+    } else if (e < 2 * cr + c) {
+      const int i = (int)(e - 2 * cr);
+      for (int n = 0; n < n_img; ++n) s += dz[(int64_t)n * c + i];
+      db2[i] = s;
+    } else {
+      const int j = (int)(e - 2 * cr - c);
+      for (int n = 0; n < n_img; ++n) s += dh[(int64_t)n * red + j];
+      db1[j] = s;
+    }
   }
 }
 
@@ -671,22 +741,38 @@ void launch_eltwise(const float* a, const float* b, float* y, int64_t n, hipStre
 
 extern "C" {
 
+long long ast_mbt_gemm_workspace_floats(int M, int N, int batch, int ksplit, long long sCb) {
+  if (M <= 0 || N <= 0 || batch <= 0 || ksplit <= 0) return 0;
+  const bool part = ksplit > 1 || (sCb == 0 && batch > 1);
+  return part ? (long long)batch * ksplit * M * N : 0;
+}
+
 int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int K, int batch, long long sAb,
                      long long sAm, long long sAk, long long sBb, long long sBk, long long sBn, long long sCb,
-                     long long sCm, long long sCn, int ksplit, int accumulate, int atomic, int foldK, int foldN,
-                     void* stream) {
+                     long long sCm, long long sCn, int ksplit, int accumulate, int foldK, int foldN,
+                     float* workspace, long long workspace_floats, void* stream) {
   if (!A || !B || !C) return AST_E_NULLPTR;
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || ksplit <= 0 || foldK < 0 || foldN < 0) return AST_E_SHAPE;
   if (((int64_t)M + GT - 1) / GT > 65535 || (int64_t)batch * ksplit > 65535) return AST_E_SHAPE;
   if ((foldK || foldN) && (batch != 1 || (foldK && foldN))) return AST_E_SHAPE;
   if (foldK && (sAk != 1 || sBk != 1 || K % foldK)) return AST_E_UNSUPPORTED;  // both operands k-contiguous
   if (foldN && (sBn != 1 || N % foldN)) return AST_E_UNSUPPORTED;
-  if (ksplit > 1 || (sCb == 0 && batch > 1)) atomic = 1;  // partial sums meet in C
-  GemmArgs a{A, B, C, sAb, sAm, sAk, sBb, sBk, sBn, sCb, sCm, sCn, M, N, K, batch, ksplit, 0, accumulate, atomic,
-             foldK, foldN};
+  const long long need = ast_mbt_gemm_workspace_floats(M, N, batch, ksplit, sCb);
+  if (need > 0 && !workspace) return AST_E_NULLPTR;
+  if (workspace_floats < need) return AST_E_SHAPE;
+  GemmArgs a{A, B, C, need > 0 ? workspace : nullptr, sAb, sAm, sAk, sBb, sBk, sBn, sCb, sCm, sCn, M, N, K, batch,
+             ksplit, 0, accumulate, foldK, foldN};
   a.kchunk = ((K + ksplit - 1) / ksplit + GK - 1) / GK * GK;
+  hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)((N + GT - 1) / GT), (unsigned)((M + GT - 1) / GT), (unsigned)(batch * ksplit));
-  hipLaunchKernelGGL(gemm_kernel, grid, dim3(kT), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(gemm_kernel, grid, dim3(kT), 0, st, a);
+  if (need > 0) {  // the partial tiles, summed in (image, split) order
+    const bool shared = sCb == 0 && batch > 1;
+    const int cimgs = shared ? 1 : batch;
+    const int zper = shared ? batch * ksplit : ksplit;
+    const int64_t mn = (int64_t)M * N;
+    hipLaunchKernelGGL(gemm_reduce_kernel, dim3(grid_for(mn, 8192), (unsigned)cimgs), dim3(kT), 0, st, a, zper);
+  }
   return (int)hipGetLastError();
 }
 
@@ -700,12 +786,14 @@ int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int
 
 long long ast_mbt_dw_workspace_floats(int n, int c, int h, int wd, int k) {
   if (n <= 0 || c <= 0 || h <= 0 || wd <= 0 || (k != 3 && k != 5)) return 0;
-  return (long long)n * c * (h + k - 1) * (wd + k - 1);
+  const long long dpad = (long long)n * c * (h + k - 1) * (wd + k - 1);            // mode 1
+  const long long wpart = (long long)c * n * ((h * wd + DW_SEG - 1) / DW_SEG) * k * k;  // mode 2 (stride 1 bound)
+  return dpad > wpart ? dpad : wpart;
 }
 
 int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, float* out, int n, int c, int h, int wd,
                    int k, int s, float* workspace, long long workspace_floats, void* stream) {
-  if (!w || !out || (mode != 1 && !x) || (mode != 0 && !g) || (mode == 1 && !workspace)) return AST_E_NULLPTR;
+  if (!w || !out || (mode != 1 && !x) || (mode != 0 && !g) || (mode != 0 && !workspace)) return AST_E_NULLPTR;
   if (n <= 0 || c <= 0 || h <= 0 || wd <= 0 || (k != 3 && k != 5) || (s != 1 && s != 2)) return AST_E_SHAPE;
   const int p = (k - 1) / 2;
   if (p >= h || p >= wd) return AST_E_SHAPE;  // reflect padding needs pad < size
@@ -727,10 +815,13 @@ int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, flo
       hipLaunchKernelGGL(dw_fold_kernel<2>, dim3((h * wd + kT - 1) / kT, gy), dim3(kT), 0, st, workspace, out, (int)nc,
                          h, wd);
   } else {
-    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)c * k * k, st);
+    const int segs = (ho * wo + DW_SEG - 1) / DW_SEG;
+    const int64_t rows = (int64_t)n * segs;  // partials per channel: (image, segment) rows of k*k
+    if (workspace_floats < (long long)c * rows * k * k) return AST_E_SHAPE;  // workspace too small
+    const dim3 grid((unsigned)segs, (unsigned)n, (unsigned)c);
+    AST_DW_DISPATCH(dw_wgrad_kernel, grid, x, g, workspace, c, h, wd, ho, wo);
+    const hipError_t e = ast_det::reduce_cols(workspace, rows, k * k, k * k, c, rows * k * k, out, k * k, false, st);
     if (e != hipSuccess) return (int)e;
-    const dim3 grid((unsigned)((ho * wo + DW_SEG - 1) / DW_SEG), (unsigned)n, (unsigned)c);
-    AST_DW_DISPATCH(dw_wgrad_kernel, grid, x, g, out, c, h, wd, ho, wo);
   }
   return (int)hipGetLastError();
 }
@@ -891,17 +982,17 @@ int ast_mbt_se_fc_fwd_f32(const float* pool, const float* w1, const float* b1, c
 
 int ast_mbt_se_fc_bwd_f32(const float* dgate, const float* z, const float* hid, const float* pool, const float* w1,
                           const float* w2, int n, int c, int red, long long hw, float* dw1, float* db1, float* dw2,
-                          float* db2, float* dpool, void* stream) {
-  if (!dgate || !z || !hid || !pool || !w1 || !w2 || !dw1 || !db1 || !dw2 || !db2 || !dpool) return AST_E_NULLPTR;
+                          float* db2, float* dpool, float* workspace, long long workspace_floats, void* stream) {
+  if (!dgate || !z || !hid || !pool || !w1 || !w2 || !dw1 || !db1 || !dw2 || !db2 || !dpool || !workspace)
+    return AST_E_NULLPTR;
   if (n <= 0 || c <= 0 || red <= 0 || hw <= 0 || c + red > 16384) return AST_E_SHAPE;
+  if (workspace_floats < (long long)n * (c + red)) return AST_E_SHAPE;
   hipStream_t st = (hipStream_t)stream;
-  hipError_t e;
-  if ((e = hipMemsetAsync(dw1, 0, sizeof(float) * (size_t)red * c, st)) != hipSuccess) return (int)e;
-  if ((e = hipMemsetAsync(dw2, 0, sizeof(float) * (size_t)red * c, st)) != hipSuccess) return (int)e;
-  if ((e = hipMemsetAsync(db1, 0, sizeof(float) * (size_t)red, st)) != hipSuccess) return (int)e;
-  if ((e = hipMemsetAsync(db2, 0, sizeof(float) * (size_t)c, st)) != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(n), dim3(kT), sizeof(float) * (c + red), st, dgate, z, hid, pool, w1, w2, c,
-                     red, 1.0f / (float)hw, dw1, db1, dw2, db2, dpool);
+  hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(n), dim3(kT), sizeof(float) * (c + red), st, dgate, z, hid, w1, w2, n, c,
+                     red, 1.0f / (float)hw, workspace, dpool);
+  const int64_t total = 2LL * c * red + c + red;
+  hipLaunchKernelGGL(se_fc_param_grad_kernel, dim3(grid_for(total, 4096)), dim3(kT), 0, st, workspace, hid, pool, n,
+                     c, red, dw1, db1, dw2, db2);
   return (int)hipGetLastError();
 }
 

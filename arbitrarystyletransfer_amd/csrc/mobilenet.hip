@@ -23,6 +23,7 @@
 #include <stdlib.h>
 #include "../../include/ast_hip.h"
 #include "mb_common.h"
+#include "det.h"
 
 namespace {
 
@@ -375,7 +376,7 @@ __global__ __launch_bounds__(kThreads, 2) void expand_dw_kernel(EdArgs a) {
       }
 #pragma unroll
       for (int o = 8; o > 0; o >>= 1) psum += __shfl_xor(psum, o, 64);
-      if ((tid & 15) == 0) atomicAdd(a.pool + (int64_t)n * a.hid + hc, psum);
+      if ((tid & 15) == 0) a.pool[((int64_t)n * a.hid + hc) * a.slots + ty * a.tiles_x + tx] = psum;
     }
     lds_barrier();  // hs / ws reused by the next chunk
   }
@@ -458,8 +459,7 @@ __global__ __launch_bounds__(NT_, 4) void expand_dw2_kernel(EdArgs a) {  // 4 wa
   float* pool_s = reinterpret_cast<float*>(ring + 4 * sl.bytes);              // [hid] this tile's SE sums
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // image index fastest: co-resident workgroups belong to different images, so their SE-pool
-  // atomics (one per channel per tile) do not pile onto the same few addresses
+  // image index fastest: co-resident workgroups belong to different images
   const int n = blockIdx.x % a.n;
   int b = blockIdx.x / a.n;
   const int tx = b % a.tiles_x;
@@ -694,7 +694,7 @@ __global__ __launch_bounds__(NT_, 4) void expand_dw2_kernel(EdArgs a) {  // 4 wa
     }
 #pragma unroll
     for (int o = TPC / 2; o > 0; o >>= 1) psum += __shfl_xor(psum, o, 64);
-    if ((tid % TPC) == 0) pool_s[hc] = psum;  // each channel once per tile: one coalesced atomic pass at the end
+    if ((tid % TPC) == 0) pool_s[hc] = psum;  // each channel once per tile: stored at the end
   };
 
   // ---- prologue: parameters of chunks 0 and 1 in slots, chunk 2's in flight, chunk 0's image ----
@@ -723,7 +723,7 @@ __global__ __launch_bounds__(NT_, 4) void expand_dw2_kernel(EdArgs a) {  // 4 wa
     lds_barrier();
   }
   if (!(ED2_SKIP & 8))
-    for (int c = tid; c < a.hid; c += NT) atomicAdd(a.pool + (int64_t)n * a.hid + c, pool_s[c]);
+    for (int c = tid; c < a.hid; c += NT) a.pool[((int64_t)n * a.hid + c) * a.slots + b] = pool_s[c];
 #undef ED2_FETCH
 #undef ED2_STASH
 #undef ED2_ROTATE
@@ -835,7 +835,7 @@ __global__ __launch_bounds__(NT_, OCC) void expand_dw3_kernel(EdArgs a) {
   float* pool_s = reinterpret_cast<float*>(smem + L.pool);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n = blockIdx.x % a.n;  // image fastest (SE-pool atomics spread over images)
+  const int n = blockIdx.x % a.n;  // image fastest
   const int b = blockIdx.x / a.n;
   const int tx = b % a.tiles_x, ty = b / a.tiles_x;
   const int oy0 = ty * G::TH, ox0 = tx * G::TW;
@@ -1020,8 +1020,10 @@ __global__ __launch_bounds__(NT_, OCC) void expand_dw3_kernel(EdArgs a) {
             }
         }
       }
-      psum = row_sum_dpp(psum);  // every lane: its 16-lane row's sum; one LDS add per row
-      if (r16 == 0) __hip_atomic_fetch_add(pool_s + hc, psum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      psum = row_sum_dpp(psum);  // every lane: its 16-lane row's sum
+      // the wave's four rows in a fixed order (this wave alone owns channel hc of the tile)
+      psum = (__shfl(psum, 0, 64) + __shfl(psum, 16, 64)) + (__shfl(psum, 32, 64) + __shfl(psum, 48, 64));
+      if (lane == 0) pool_s[hc] = psum;
     }
   };
 
@@ -1049,7 +1051,7 @@ __global__ __launch_bounds__(NT_, OCC) void expand_dw3_kernel(EdArgs a) {
     depthwise(c + 1, hs1);
     lds_barrier();
   }
-  for (int c = tid; c < a.hid; c += NT) atomicAdd(a.pool + (int64_t)n * a.hid + c, pool_s[c]);
+  for (int c = tid; c < a.hid; c += NT) a.pool[((int64_t)n * a.hid + c) * a.slots + b] = pool_s[c];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1525,6 +1527,7 @@ int launch_ed_th(EdArgs a, hipStream_t st) {
   a.tiles_y = (a.ho + TH - 1) / TH;
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.n;
   if (blocks > 0x7fffffffLL) return AST_E_SHAPE;
+  if (ed_plan(a, (int64_t)a.tiles_x * a.tiles_y)) return 0;
   const size_t lds = ed_lds_bytes<T, K, S, TH, TW>(a.cin_pad, EXPAND);
   auto kern = expand_dw_kernel<T, K, S, UP, EXPAND, TH, TW>;
   if (lds > 64 * 1024) {
@@ -1565,6 +1568,7 @@ int launch_ed2(EdArgs a, hipStream_t st) {
   a.tiles_y = (a.ho + TH - 1) / TH;
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.n;
   if (blocks > 0x7fffffffLL) return AST_E_SHAPE;
+  if (ed_plan(a, (int64_t)a.tiles_x * a.tiles_y)) return 0;
   const size_t lds = ed2_lds_bytes<K, TH, TW, R, NT>(a.cin_pad, EXPAND, a.hid);
   auto kern = expand_dw2_kernel<K, UP, EXPAND, TH, TW, R, NT>;
   const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1600,6 +1604,7 @@ int launch_ed3(EdArgs a, hipStream_t st) {
   a.tiles_y = (a.ho + G::TH - 1) / G::TH;
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.n;
   if (blocks > 0x7fffffffLL) return AST_E_SHAPE;
+  if (ed_plan(a, (int64_t)a.tiles_x * a.tiles_y)) return 0;
   // two 8-wave workgroups per CU when the LDS allows, else one 16-wave workgroup (latency hiding)
   const bool two = lds <= kLdsBudget;
   const int nt = g_ed3_nt ? g_ed3_nt : two ? 512 : 1024;
@@ -1692,17 +1697,16 @@ int launch_dense(const void* x, const float* w, const float* b, void* y, int n, 
 
 }  // namespace
 
-extern "C" {
-
-int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, int cin, int h, int w, int up,
-                     const void* w1p, const float* b1, int hid, int cin_pad, const float* wdw, const float* bdw,
-                     int k, int stride, void* d, float* pool, int ho, int wo, void* stream) {
-  if (!x1 || !wdw || !bdw || !d || !pool) return AST_E_NULLPTR;
-  if (w1p && !b1) return AST_E_NULLPTR;
+namespace {
+// Argument checks and EdArgs of ast_mb_expand_dw (shared with its workspace query).
+int ed_setup(int dtype, const void* x1, const void* x2, int c1, int n, int cin, int h, int w, int up, const void* w1p,
+             int hid, int cin_pad, int k, int stride, int ho, int wo, EdArgs* out) {
   if (n <= 0 || cin <= 0 || h <= 1 || w <= 1 || hid <= 0 || ho <= 0 || wo <= 0) return AST_E_SHAPE;
   if (up != 1 && up != 2) return AST_E_SHAPE;
   if (!x2) { x2 = x1; c1 = cin; }
   if (c1 <= 0 || c1 > cin) return AST_E_SHAPE;
+  if (k != 3 && k != 5) return AST_E_UNSUPPORTED;
+  if (stride != 1 && stride != 2) return AST_E_UNSUPPORTED;
   const int p = (k - 1) / 2;
   if ((h * up + 2 * p - k) / stride + 1 != ho || (w * up + 2 * p - k) / stride + 1 != wo) return AST_E_SHAPE;
   if (h * up <= p || w * up <= p) return AST_E_SHAPE;  // reflection pad needs pad < size
@@ -1713,7 +1717,7 @@ int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, i
   } else if (hid != cin) {
     return AST_E_SHAPE;
   }
-  hipStream_t st = (hipStream_t)stream;
+  if (dtype != 0 && dtype != 1) return AST_E_UNSUPPORTED;
   static const int ver = [] {
     const char* v = getenv("AST_MB_ED");
     return v ? atoi(v) : 4;
@@ -1734,12 +1738,56 @@ int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, i
     return v ? atoi(v) : 0;
   }();
   g_ed3_nt = ed3_nt;
-  hipError_t e = hipMemsetAsync(pool, 0, sizeof(float) * (size_t)n * hid, st);
-  if (e != hipSuccess) return (int)e;
-    EdArgs a{x1, x2, c1, n, cin, h, w, h * up, w * up, ho, wo, w1p, b1, hid, expand ? cin_pad : 0, wdw, bdw, d, pool, 0, 0};
+  *out = EdArgs{x1, x2, c1, n, cin, h, w, h * up, w * up, ho, wo, w1p, nullptr, hid, expand ? cin_pad : 0,
+                nullptr, nullptr, nullptr, nullptr, 0, 0, 0, nullptr};
+  return 0;
+}
+
+int ed_dispatch(int dtype, EdArgs a, int k, int stride, int up, hipStream_t st) {
+  const bool expand = a.w1 != nullptr;
   if (dtype == 0) return dispatch_ed<float>(a, k, stride, up, expand, st);
-  if (dtype == 1) return dispatch_ed<bf16>(a, k, stride, up, expand, st);
-  return AST_E_UNSUPPORTED;
+  return dispatch_ed<bf16>(a, k, stride, up, expand, st);
+}
+}  // namespace
+
+extern "C" {
+
+long long ast_mb_expand_dw_workspace_floats(int dtype, int has_x2, int c1, int n, int cin, int h, int w, int up,
+                                            int expand, int hid, int cin_pad, int k, int stride, int ho, int wo) {
+  static const char dummy = 0;  // stand-in pointers: the plan only looks at their presence
+  EdArgs a;
+  if (ed_setup(dtype, &dummy, has_x2 ? &dummy : nullptr, c1, n, cin, h, w, up, expand ? &dummy : nullptr, hid,
+               cin_pad, k, stride, ho, wo, &a))
+    return 0;
+  long long slots = 0;
+  a.plan = &slots;
+  if (ed_dispatch(dtype, a, k, stride, up, nullptr) != 0 || slots <= 0) return 0;
+  return (long long)n * hid * slots;
+}
+
+int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, int cin, int h, int w, int up,
+                     const void* w1p, const float* b1, int hid, int cin_pad, const float* wdw, const float* bdw,
+                     int k, int stride, void* d, float* pool, int ho, int wo, float* workspace,
+                     long long workspace_floats, void* stream) {
+  if (!x1 || !wdw || !bdw || !d || !pool || !workspace) return AST_E_NULLPTR;
+  if (w1p && !b1) return AST_E_NULLPTR;
+  EdArgs a;
+  if (const int e = ed_setup(dtype, x1, x2, c1, n, cin, h, w, up, w1p, hid, cin_pad, k, stride, ho, wo, &a)) return e;
+  hipStream_t st = (hipStream_t)stream;
+  long long slots = 0;
+  a.plan = &slots;
+  if (const int e = ed_dispatch(dtype, a, k, stride, up, st)) return e;
+  if (slots <= 0 || slots > 0x7fffffff) return AST_E_UNSUPPORTED;
+  if (workspace_floats < (long long)n * hid * slots) return AST_E_SHAPE;  // workspace too small
+  a.plan = nullptr;
+  a.b1 = b1;
+  a.wdw = wdw;
+  a.bdw = bdw;
+  a.d = d;
+  a.pool = workspace;  // [n][hid][slots] tile sums
+  if (const int e = ed_dispatch(dtype, a, k, stride, up, st)) return e;
+  // pool[n][c] = the channel's tile sums in tile order
+  return (int)ast_det::reduce_rows(workspace, (int64_t)n * hid, (int)slots, pool, st);
 }
 
 int ast_mb_se_fold(int dtype, const float* pool, int n, int hid, long long hw, const float* fc1w,

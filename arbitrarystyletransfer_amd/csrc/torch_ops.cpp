@@ -9,6 +9,7 @@
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
 
 #include <tuple>
 
@@ -44,13 +45,20 @@ at::Tensor dev_f32(const at::Tensor& t, const char* name) {
 
 const float* fptr(const c10::optional<at::Tensor>& t) { return t ? t->data_ptr<float>() : nullptr; }
 
+// Every tensor argument of an op must live on the device of its first input (whose stream the
+// launch uses): a pointer from another GPU would be read as if it were local.
+void same_device(const at::Tensor& ref, const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.device() == ref.device(), name, " is on ", t.device(), " but the op runs on ", ref.device());
+}
+
 // ---- AdaIN (models.py:43-51) + alpha blend (models.py:471) ----------------------------------
 at::Tensor adain(const at::Tensor& content_, const at::Tensor& style_, double alpha, bool swap_style_stats) {
   at::Tensor content = dev_f32(content_, "content_map"), style = dev_f32(style_, "style_map");
   TORCH_CHECK(content.dim() == 4 && style.dim() == 4 && content.size(0) == style.size(0) &&
                   content.size(1) == style.size(1),
               "AdaIN needs NCHW maps with equal (N, C): ", content.sizes(), " vs ", style.sizes());
-  TORCH_CHECK(content.device() == style.device(), "content_map and style_map on different devices");
+  same_device(content, style, "style_map");
+  const c10::hip::HIPGuard guard(content.device());
   at::Tensor out = at::empty_like(content);
   AST_CALL("adain", ast_adain_f32(content.data_ptr<float>(), style.data_ptr<float>(), out.data_ptr<float>(),
                                   (int)content.size(0), (int)content.size(1), (int)content.size(2),
@@ -70,6 +78,7 @@ at::Tensor adain_meta(const at::Tensor& content, const at::Tensor& style, double
 std::tuple<at::Tensor, at::Tensor> channel_stats(const at::Tensor& x_, bool unbiased, double eps) {
   at::Tensor x = dev_f32(x_, "x");
   TORCH_CHECK(x.dim() == 4, "channel_stats expects NCHW, got ", x.sizes());
+  const c10::hip::HIPGuard guard(x.device());
   at::Tensor mean = at::empty({x.size(0), x.size(1), 1, 1}, x.options());
   at::Tensor std_ = at::empty_like(mean);
   AST_CALL("channel_stats", ast_channel_stats_f32(x.data_ptr<float>(), mean.data_ptr<float>(), std_.data_ptr<float>(),
@@ -90,6 +99,7 @@ at::Tensor conv3x3_pack(const at::Tensor& w_) {
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "conv3x3 weight must be [cout, cin, 3, 3], got ",
               w.sizes());
   const int cout = (int)w.size(0), cin = (int)w.size(1);
+  const c10::hip::HIPGuard guard(w.device());
   at::Tensor out = at::empty({(int64_t)ast_conv3x3_packed_numel(cout, cin)}, w.options());
   AST_CALL("conv3x3_pack", ast_conv3x3_pack_weights_f32(w.data_ptr<float>(), out.data_ptr<float>(), cout, cin,
                                                         cur_stream(w)));
@@ -125,18 +135,23 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> conv3x3_fwd(
     int64_t upsample, int64_t pad_mode, const c10::optional<at::Tensor>& in_mean_,
     const c10::optional<at::Tensor>& in_std_, bool want_pre, bool want_act, bool want_pool, int64_t cfg) {
   at::Tensor x = dev_f32(x_, "x"), w_packed = dev_f32(w_packed_, "w_packed");
+  same_device(x, w_packed, "w_packed");
   const ConvShape s = conv_shape(x, w_packed, cout, upsample, pad_mode, want_pre, want_act, want_pool);
   c10::optional<at::Tensor> bias, in_mean, in_std;
   if (bias_) {
     bias = dev_f32(*bias_, "bias");
+    same_device(x, *bias, "bias");
     TORCH_CHECK(bias->numel() == cout, "bias size mismatch");
   }
   TORCH_CHECK(in_mean_.has_value() == in_std_.has_value(), "in_mean and in_std go together");
   if (in_mean_) {
     in_mean = dev_f32(*in_mean_, "in_mean");
     in_std = dev_f32(*in_std_, "in_std");
+    same_device(x, *in_mean, "in_mean");
+    same_device(x, *in_std, "in_std");
     TORCH_CHECK(in_mean->numel() == s.cin && in_std->numel() == s.cin, "normalisation stats must have cin entries");
   }
+  const c10::hip::HIPGuard guard(x.device());
   auto mk = [&](bool want, int64_t h, int64_t w) {
     return want ? at::empty({s.n, cout, h, w}, x.options()) : at::empty({0}, x.options());
   };
@@ -166,9 +181,12 @@ at::Tensor gram(const at::Tensor& f_) {
   at::Tensor f = dev_f32(f_, "tensor");
   TORCH_CHECK(f.dim() == 4, "gram_matrix expects [B, C, H, W], got ", f.sizes());
   const int64_t b = f.size(0), c = f.size(1), hw = f.size(2) * f.size(3);
+  const c10::hip::HIPGuard guard(f.device());
   at::Tensor g = at::empty({b, c, c}, f.options());
+  const long long wsf = ast_gram_workspace_floats((int)b, (int)c, hw);
+  at::Tensor ws = at::empty({wsf > 0 ? wsf : 1}, f.options());
   AST_CALL("gram", ast_gram_f32(f.data_ptr<float>(), g.data_ptr<float>(), (int)b, (int)c, hw,
-                                (float)(1.0 / (double)(c * hw)), cur_stream(f)));
+                                (float)(1.0 / (double)(c * hw)), ws.data_ptr<float>(), wsf, cur_stream(f)));
   return g;
 }
 

@@ -7,7 +7,7 @@ from __future__ import annotations
 import torch
 
 from . import ops
-from ._lib import HipOpError, check, lib, ptr, stream_ptr
+from ._lib import HipOpError, check, lib, loss_accumulator, ptr, stream_ptr, workspace
 
 _dev = ops._dev
 
@@ -87,10 +87,11 @@ def conv_weight_grad(x, dy, cout, upsample=1, pad_mode="zeros", with_bias=True, 
     db = _grad_buffer(bias, (cout,), x) if with_bias else None
     flops = 2 * n * h * upsample * w * upsample * cout * cin * 9
     pitch, plane, off = dy_layout
+    ws = workspace(lib().ast_conv3x3_wgrad_workspace_floats(n, cin, h, w, cout, upsample), x.device)
     check(ops._timed(f"wgrad {cin}->{cout} {h * upsample}x{w * upsample}", flops, x.device,
                      lambda: lib().ast_conv3x3_wgrad_ex_f32(ptr(x), ptr(dy), ptr(dw), ptr(db), n, cin, h, w, cout,
                                                             upsample, ops.PAD_MODES[pad_mode], pitch, plane, off,
-                                                            _s(x))),
+                                                            ptr(ws), ws.numel(), _s(x))),
           "conv3x3_wgrad")
     return dw, db
 
@@ -274,8 +275,23 @@ def mean_variance_norm(x):
 # Losses (scalar outputs; the backward kernels take grad_output as a device scalar)
 # ------------------------------------------------------------------------------------------------
 
-def _scalar(like):
-    return torch.zeros((), device=like.device, dtype=torch.float32)
+def _acc(like):
+    """A loss accumulator (ast_hip.h: value at [0], then the per-workgroup partials that the
+    kernels sum in a fixed order)."""
+    return loss_accumulator(like.device)
+
+
+def _value(acc):
+    """The 0-d loss value of an accumulator (a view of element 0)."""
+    return acc[0]
+
+
+def gram(f, g, scale):
+    """g[b] = scale * f[b] f[b]^T for f [b, c, hw] (the deterministic split-K launch)."""
+    b, c = int(f.shape[0]), int(f.shape[1])
+    hw = f.numel() // (b * c)
+    ws = workspace(lib().ast_gram_workspace_floats(b, c, hw), f.device)
+    check(lib().ast_gram_f32(ptr(f), ptr(g), b, c, hw, scale, ptr(ws), ws.numel(), _s(f)), "gram")
 
 
 class GramFn(torch.autograd.Function):
@@ -284,7 +300,7 @@ class GramFn(torch.autograd.Function):
         f = _dev(f, "tensor")
         b, c, h, w = f.shape
         g = _empty((b, c, c), f)
-        check(lib().ast_gram_f32(ptr(f), ptr(g), b, c, h * w, 1.0 / (c * h * w), _s(f)), "gram")
+        gram(f, g, 1.0 / (c * h * w))
         ctx.save_for_backward(f)
         return g
 
@@ -305,10 +321,10 @@ class HuberFn(torch.autograd.Function):
         x, y = _dev(x, "input"), _dev(y, "target")
         if x.shape != y.shape:
             raise HipOpError(f"huber: shape mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
-        loss = _scalar(x)
+        loss = _acc(x)
         check(lib().ast_huber_f32(ptr(x), ptr(y), x.numel(), 1.0, None, ptr(loss), None, 0, _s(x)), "huber")
         ctx.save_for_backward(x, y)
-        return loss
+        return _value(loss)
 
     @staticmethod
     def backward(ctx, g):
@@ -334,13 +350,13 @@ class MVNHuberFn(torch.autograd.Function):
         if x.shape != y.shape:
             raise HipOpError(f"content loss: shape mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
         n, c = x.shape[:2]
-        loss = _scalar(x)
+        loss = _acc(x)
         pstats = _empty((n * c, 6), x) if ctx.needs_input_grad[0] else None
         check(lib().ast_mvn_huber_f32(ptr(x), ptr(y), n * c, x[0, 0].numel(), weight, ptr(loss), ptr(pstats),
                                       _s(x)), "mvn_huber")
         ctx.save_for_backward(x, y, pstats)
         ctx.weight = weight
-        return loss
+        return _value(loss)
 
     @staticmethod
     def backward(ctx, g):
@@ -363,12 +379,12 @@ class StyleLossFn(torch.autograd.Function):
         x, y = _dev(x, "x"), _dev(y, "y")
         if x.shape[:2] != y.shape[:2]:
             raise HipOpError("style loss: (N, C) mismatch")
-        loss = _scalar(x)
+        loss = _acc(x)
         # with a gradient to come, the forward also keeps dG and the moment-term coefficients
         # (all linear in grad_output), so the backward is one GEMM with grad_output as a scale
         dg, ra, rb = _style_terms(x, y, weight, loss, want_grad=ctx.needs_input_grad[0])
         ctx.save_for_backward(x, dg, ra, rb)
-        return loss
+        return _value(loss)
 
     @staticmethod
     def backward(ctx, g):
@@ -398,8 +414,8 @@ def _style_terms(x, y, weight, loss, want_grad):
     gx = _empty((b, c, c), x)
     gy = _empty((b, c, c), x)
     scale = 1.0 / (c * hw)
-    check(L.ast_gram_f32(ptr(x), ptr(gx), b, c, hw, scale, s), "gram")
-    check(L.ast_gram_f32(ptr(y), ptr(gy), b, c, hw, scale, s), "gram")
+    gram(x, gx, scale)
+    gram(y, gy, scale)
     dg = _empty((b, c, c), x) if want_grad else None
     check(L.ast_gram_huber_f32(ptr(gx), ptr(gy), b * c * c, weight, None, ptr(loss), ptr(dg), s), "gram_huber")
     return dg, ra, rb
@@ -410,10 +426,10 @@ class TVLossFn(torch.autograd.Function):
     def forward(ctx, img):
         img = _dev(img, "img")
         n, c, h, w = img.shape
-        loss = _scalar(img)
+        loss = _acc(img)
         check(lib().ast_tv_loss_f32(ptr(img), n * c, h, w, 1.0, None, ptr(loss), None, 0, _s(img)), "tv_loss")
         ctx.save_for_backward(img)
-        return loss
+        return _value(loss)
 
     @staticmethod
     def backward(ctx, g):
@@ -438,8 +454,9 @@ def soft_histogram(x):
     x = _dev(x, "x")
     b = x.shape[0]
     hist = _empty((b, HIST_BINS), x)
-    check(lib().ast_soft_hist_f32(ptr(x), b, x.numel() // b, 1.0 / (x.shape[1] * x.shape[2]), ptr(hist), _s(x)),
-          "soft_hist")
+    ws = workspace(lib().ast_soft_hist_workspace_floats(b), x.device)
+    check(lib().ast_soft_hist_f32(ptr(x), b, x.numel() // b, 1.0 / (x.shape[1] * x.shape[2]), ptr(hist), ptr(ws),
+                                  ws.numel(), _s(x)), "soft_hist")
     return hist
 
 
@@ -453,12 +470,12 @@ class HistLossFn(torch.autograd.Function):
         if x.shape[0] != y.shape[0]:
             raise HipOpError(f"hist loss: batch mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
         hx, hy = soft_histogram(x), soft_histogram(y)
-        loss = _scalar(x)
+        loss = _acc(x)
         check(lib().ast_emd_loss_f32(ptr(hx), ptr(hy), x.shape[0], float(weight), None, ptr(loss), None, _s(x)),
               "emd_loss")
         ctx.save_for_backward(x, hx, hy)
         ctx.weight = float(weight)
-        return loss
+        return _value(loss)
 
     @staticmethod
     def backward(ctx, g):
@@ -479,12 +496,12 @@ class RangeLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight):
         x = _dev(x, "x")
-        loss = _scalar(x)
+        loss = _acc(x)
         check(lib().ast_range_loss_f32(ptr(x), x.numel(), float(weight), None, ptr(loss), None, 0, _s(x)),
               "range_loss")
         ctx.save_for_backward(x)
         ctx.weight = float(weight)
-        return loss
+        return _value(loss)
 
     @staticmethod
     def backward(ctx, g):
@@ -503,12 +520,12 @@ class SqDiffMeanFn(torch.autograd.Function):
         x, y = _dev(x, "x"), _dev(y, "y")
         if x.shape != y.shape:
             raise HipOpError(f"sqdiff: shape mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
-        loss = _scalar(x)
+        loss = _acc(x)
         check(lib().ast_sqdiff_mean_f32(ptr(x), ptr(y), x.numel(), float(weight), None, ptr(loss), None, 0, _s(x)),
               "sqdiff")
         ctx.save_for_backward(x, y)
         ctx.weight = float(weight)
-        return loss
+        return _value(loss)
 
     @staticmethod
     def backward(ctx, g):

@@ -14,7 +14,7 @@ import torch
 import torch.nn as nn
 
 from . import dp, ops
-from ._lib import HipOpError, check, lib, ptr, stream_ptr
+from ._lib import HipOpError, check, lib, ptr, stream_ptr, workspace
 
 
 def _s(t):
@@ -31,15 +31,18 @@ def _f32(t, name):
 
 def gemm(A, B, C, M, N, K, batch, sA, sB, sC, ksplit=1, accumulate=False, fold_k=0, fold_n=0, role=""):
     """C[b][m][n] (+)= sum_k A[b][m][k] B[b][k][n]; sA/sB/sC = (batch, row, col) element strides.
-    fold_n / fold_k = P: the image index is folded into N / K (batch 1; see ast_hip.h)."""
+    fold_n / fold_k = P: the image index is folded into N / K (batch 1; see ast_hip.h). K-split or
+    batch-shared C tiles meet in a workspace and are summed in a fixed order (deterministic)."""
+    nws = int(lib().ast_mbt_gemm_workspace_floats(M, N, batch, ksplit, sC[0]))
+    ws = workspace(nws, C.device) if nws > 0 else None
     check(ops._timed(f"mbgemm {role} {M}x{N}x{K}", 2 * M * N * K * batch, C.device, lambda: lib().ast_mbt_gemm_f32(
-        ptr(A), ptr(B), ptr(C), M, N, K, batch, *sA, *sB, *sC, ksplit, int(accumulate), 0, fold_k, fold_n, _s(C))),
-        "gemm")
+        ptr(A), ptr(B), ptr(C), M, N, K, batch, *sA, *sB, *sC, ksplit, int(accumulate), fold_k, fold_n, ptr(ws),
+        nws, _s(C))), "gemm")
 
 
 def _ksplit(m, n, k):
     """Split the weight gradient's long reduction so ~1024 workgroups run (4 per CU), chunks >= 256
-    deep; the partial tiles meet in C through atomics."""
+    deep; the partial tiles meet in the workspace and are summed in split order."""
     tiles = -(-m // 64) * -(-n // 64)
     return max(1, min(-(-1024 // tiles), k // 256, 65535))
 
@@ -90,7 +93,7 @@ class PwConvFn(torch.autograd.Function):
         if ctx.has_x2:
             dx2 = grads[1]
         if ctx.needs_input_grad[2]:
-            dw = torch.zeros((cout, cin), device=g.device, dtype=torch.float32)
+            dw = torch.empty((cout, cin), device=g.device, dtype=torch.float32)
             for xi, off in parts:
                 ci = xi.shape[1]
                 gemm(g, xi, dw[:, off:], cout, ci, n * P, 1, (cout * P, P, 1), (ci * P, 1, P), (0, cin, 1),
@@ -129,8 +132,9 @@ class DwConvFn(torch.autograd.Function):
                                        _s(g)), "dw dgrad")
         if ctx.needs_input_grad[1]:
             dw = torch.empty((c, ctx.k * ctx.k), device=g.device, dtype=torch.float32)
-            check(lib().ast_mbt_dw_f32(2, ptr(x), ptr(wt), ptr(g), ptr(dw), n, c, h, w, ctx.k, ctx.s, None, 0, _s(g)),
-                  "dw wgrad")
+            ws = workspace(lib().ast_mbt_dw_workspace_floats(n, c, h, w, ctx.k), x.device)
+            check(lib().ast_mbt_dw_f32(2, ptr(x), ptr(wt), ptr(g), ptr(dw), n, c, h, w, ctx.k, ctx.s, ptr(ws), ws.numel(),
+                                       _s(g)), "dw wgrad")
             dw = dw.reshape(ctx.wshape)
         return dx, dw, None, None
 
@@ -288,8 +292,10 @@ class SEFn(torch.autograd.Function):
         dw1, db1 = torch.empty_like(w1), torch.empty((red,), device=x.device, dtype=torch.float32)
         dw2, db2 = torch.empty_like(w2), torch.empty((c,), device=x.device, dtype=torch.float32)
         dpool = torch.empty((n, c), device=x.device, dtype=torch.float32)
+        ws = workspace(n * (c + red), x.device)
         check(lib().ast_mbt_se_fc_bwd_f32(ptr(dgate), ptr(z), ptr(hid), ptr(pool), ptr(w1), ptr(w2), n, c, red, h * w,
-                                          ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), ptr(dpool), _s(g)), "se fc bwd")
+                                          ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), ptr(dpool), ptr(ws), ws.numel(),
+                                          _s(g)), "se fc bwd")
         dx = torch.empty_like(x)
         check(lib().ast_mbt_plane_f32(2, ptr(g), None, ptr(gate), ptr(dpool), ptr(dx), n * c, h * w, _s(g)),
               "se dx")

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import mbtrain, ops
-from ._lib import HipOpError, check, lib, ptr, stream_ptr
+from ._lib import HipOpError, check, lib, ptr, stream_ptr, workspace
 
 __all__ = ["_make_divisible", "conv_3x3_bn", "SELayer", "DepthWiseConv"]
 
@@ -61,8 +61,23 @@ def act_dtype(module: nn.Module) -> torch.dtype:
 
 def check_inference(x: torch.Tensor, module: nn.Module) -> None:
     if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in module.parameters())):
-        raise NotImplementedError("the MobileNet-variant HIP path is inference-only (SURVEY.md §8a A7-A9): "
-                                  "run it under torch.no_grad() or torch.inference_mode()")
+        raise NotImplementedError("the fused MobileNet-variant kernels fold eval-mode BatchNorm and keep no "
+                                  "intermediates for autograd; this module has eval-mode BatchNorm under autograd: "
+                                  "run it under torch.no_grad(), or in train mode (mbtrain.py training kernels)")
+
+
+_ED_WS = {}
+
+
+def _expand_dw(dt, x1, x2, c1, n, cin, h, w, up, w1p, b1, hid, cin_pad, wd, bd, k, s, d, pool, ho, wo, st):
+    """ast_mb_expand_dw with its workspace (the per-tile SE-pool sums, reduced in tile order)."""
+    key = (DTYPE_CODE[dt], x2 is not None, c1, n, cin, h, w, up, w1p is not None, hid, cin_pad, k, s, ho, wo)
+    nws = _ED_WS.get(key)
+    if nws is None:
+        nws = _ED_WS[key] = int(lib().ast_mb_expand_dw_workspace_floats(*(int(v) for v in key)))
+    ws = workspace(nws, d.device)
+    return lib().ast_mb_expand_dw(DTYPE_CODE[dt], ptr(x1), ptr(x2), c1, n, cin, h, w, up, ptr(w1p), ptr(b1), hid,
+                                  cin_pad, ptr(wd), ptr(bd), k, s, ptr(d), ptr(pool), ho, wo, ptr(ws), ws.numel(), st)
 
 
 def _act_input(x: torch.Tensor, dt: torch.dtype, name: str = "x") -> torch.Tensor:
@@ -297,15 +312,13 @@ class DepthWiseConv(nn.Module):
                                  DTYPE_CODE[dt], ptr(x), ptr(x2), c1, n, cin, h, w, ptr(p.w1p), ptr(p.b1), hid,
                                  p.cin_pad, ptr(hmid), st)), "DepthWiseConv expand GEMM")
             check(ops._timed(tag + " dw", -es * (hmid.numel() + d.numel()), dev,
-                             lambda: lib().ast_mb_expand_dw(
-                                 DTYPE_CODE[dt], ptr(hmid), None, hid, n, hid, h, w, 1, None, None, hid, 0,
-                                 ptr(p.wd), ptr(p.bd), k, s, ptr(d), ptr(pool), ho, wo, st)),
+                             lambda: _expand_dw(dt, hmid, None, hid, n, hid, h, w, 1, None, None, hid, 0, p.wd, p.bd,
+                                                k, s, d, pool, ho, wo, st)),
                   "DepthWiseConv dw")
         else:
             check(ops._timed(tag, -nb1, dev,
-                             lambda: lib().ast_mb_expand_dw(
-                                 DTYPE_CODE[dt], ptr(x), ptr(x2), c1, n, cin, h, w, up, ptr(p.w1p), ptr(p.b1), hid,
-                                 p.cin_pad, ptr(p.wd), ptr(p.bd), k, s, ptr(d), ptr(pool), ho, wo, st)),
+                             lambda: _expand_dw(dt, x, x2, c1, n, cin, h, w, up, p.w1p, p.b1, hid, p.cin_pad, p.wd,
+                                                p.bd, k, s, d, pool, ho, wo, st)),
                   "DepthWiseConv expand+dw")
         wg = torch.empty((n, p.cout_pad, p.hid_pad), device=dev, dtype=dt)
         check(lib().ast_mb_se_fold(DTYPE_CODE[dt], ptr(pool), n, hid, ho * wo, ptr(p.fc1w), ptr(p.fc1b), p.red,

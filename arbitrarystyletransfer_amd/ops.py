@@ -341,8 +341,9 @@ def emd_rows(hx: torch.Tensor, hy: torch.Tensor):
     if hx.dim() != 2 or hx.shape != hy.shape or hx.shape[1] != 256:
         raise HipOpError(f"earth movers: expected two [B, 256] tensors, got {tuple(hx.shape)} / {tuple(hy.shape)}")
     b = hx.shape[0]
-    out = torch.zeros((b,), device=hx.device, dtype=torch.float32)
+    acc_n = int(lib().ast_loss_acc_floats())
+    accs = torch.zeros((b, acc_n), device=hx.device, dtype=torch.float32)   # one loss accumulator per row
     for i in range(b):   # one scalar per row: the kernel accumulates weight/n * row sums
-        check(lib().ast_emd_loss_f32(ptr(hx[i:i + 1]), ptr(hy[i:i + 1]), 1, 1.0, None, ptr(out[i:i + 1]), None,
+        check(lib().ast_emd_loss_f32(ptr(hx[i:i + 1]), ptr(hy[i:i + 1]), 1, 1.0, None, ptr(accs[i]), None,
                                      stream_ptr(hx.device)), "emd")
-    return out
+    return accs[:, 0]

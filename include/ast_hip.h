@@ -9,6 +9,12 @@
  * `stream` is a hipStream_t passed as void*; no call allocates, copies to host or synchronises,
  * so every call is legal inside hipGraph capture. Return value: 0 on success, a negative
  * AST_E* code for an argument error (nothing launched), or a positive hipError_t.
+ *
+ * Determinism: every result is bitwise reproducible run to run on the same device and shapes.
+ * No floating-point partial sum meets another through an atomic: reductions split across
+ * workgroups write their partials into a caller-provided `workspace` (size from the matching
+ * *_workspace_floats query; device memory, 16-byte aligned) and are summed in a fixed order, and
+ * scalar losses accumulate into a loss accumulator (below).
  */
 #ifndef AST_HIP_H
 #define AST_HIP_H
@@ -26,6 +32,14 @@ extern "C" {
 
 /* Library version / capability string (e.g. "ast_hip 0.1 gfx950"). */
 const char* ast_version(void);
+
+/* Loss accumulator: AST_LOSS_ACC_FLOATS device floats, zeroed once by the caller. [0] holds the
+ * accumulated value; [1] is an arrival counter that every launch leaves at 0; [2..] hold one
+ * partial per workgroup of the running launch, summed in workgroup order by the last workgroup
+ * to finish. One stream at a time per accumulator. */
+#define AST_LOSS_SLOTS 4096
+#define AST_LOSS_ACC_FLOATS (2 + AST_LOSS_SLOTS)
+int ast_loss_acc_floats(void);
 
 /* ---------------------------------------------------------------------------------------------
  * 3x3 convolution, stride 1, "same" size, as an MFMA-fp32 implicit GEMM.
@@ -146,29 +160,35 @@ int ast_grad_pad_f32(const float* g, const float* mask, float* out_pad, long lon
 int ast_pad_up_adjoint_f32(const float* dp_full, float* dx, long long planes, int h_in, int w_in,
                            int upsample, int pitch, void* stream);
 
-/* dw [cout, cin, 3, 3] = sum over images/pixels of dy x pad(upsample(x)) (zeroed here, MFMA
- * fp32, split over pixel tiles with fp32 atomics); db [cout] = sum of dy (optional). */
+/* dw [cout, cin, 3, 3] = sum over images/pixels of dy x pad(upsample(x)) (overwritten; split-bf16
+ * MFMA, split over pixel tiles: each split's partial dW/db goes to the workspace, then one ordered
+ * reduce); db [cout] = sum of dy (optional). workspace: ast_conv3x3_wgrad_workspace_floats floats. */
+long long ast_conv3x3_wgrad_workspace_floats(int n, int cin, int h_in, int w_in, int cout, int upsample);
 int ast_conv3x3_wgrad_f32(const float* x, const float* dy, float* dw, float* db,
                           int n, int cin, int h_in, int w_in, int cout,
-                          int upsample, int pad_mode, void* stream);
+                          int upsample, int pad_mode, float* workspace, long long workspace_floats,
+                          void* stream);
 
 /* Same with dy read through (pitch, plane stride, offset of element (0,0)) — e.g. the padded
  * gradient buffer of ast_grad_pad_f32 (pitch, (h+2)*pitch, pitch+1). dy_pitch = 0: dense. */
 int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* db,
                              int n, int cin, int h_in, int w_in, int cout, int upsample,
                              int pad_mode, int dy_pitch, long long dy_plane, long long dy_offset,
-                             void* stream);
+                             float* workspace, long long workspace_floats, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
- * Losses (losses.py). Loss values are ADDED into the device scalar `loss` (may be NULL);
- * gradients are written (accumulate=0) or added (accumulate=1) into `dx` (may be NULL = value
- * only). `weight` multiplies both; `gscale` (device scalar or NULL) multiplies the gradient only
- * (autograd's grad_output).
+ * Losses (losses.py). Loss values are ADDED into the loss accumulator `loss` (AST_LOSS_ACC_FLOATS
+ * floats, value at [0]; may be NULL); gradients are written (accumulate=0) or added
+ * (accumulate=1) into `dx` (may be NULL = value only). `weight` multiplies both; `gscale` (device
+ * scalar or NULL) multiplies the gradient only (autograd's grad_output).
  * ------------------------------------------------------------------------------------------ */
 
 /* gram_matrix (losses.py:105-109): gram[b] = scale * feat[b] feat[b]^T, feat [n, c, hw],
- * gram [n, c, c] (zeroed here; split-K MFMA with fp32 atomics). */
-int ast_gram_f32(const float* feat, float* gram, int n, int c, long long hw, float scale, void* stream);
+ * gram [n, c, c] (overwritten; split-K MFMA, the K-splits' partial tiles summed in order through
+ * the workspace of ast_gram_workspace_floats floats, 0 when the launch needs no split). */
+long long ast_gram_workspace_floats(int n, int c, long long hw);
+int ast_gram_f32(const float* feat, float* gram, int n, int c, long long hw, float scale, float* workspace,
+                 long long workspace_floats, void* stream);
 
 /* dfeat[b] (+)= scale * (dgram[b] + dgram[b]^T) feat[b] + row_a[b,i] * feat[b,i,:] + row_b[b,i]
  * (the backward of gram_matrix, with compute_style_loss's mean/std gradients fused: row_a/row_b
@@ -255,14 +275,19 @@ int ast_adam_step_f32(const void* dev_table, int ntensors, long long nchunks, co
  * (w1p != NULL: packed [round_up(hid,16)][cin_pad] in dtype, cin_pad a multiple of 16 (bf16) or 4
  * (fp32), zero padded; b1 [hid]) + Hardswish, then the depthwise k x k conv (k 3|5, stride 1|2,
  * reflect pad (k-1)/2; wdw [hid][k*k], bdw [hid]) + Hardswish, written to d [n][hid][ho][wo];
- * pool [n][hid] receives the per-plane sums of d (zeroed here). w1p == NULL is the ratio-1 form
+ * pool [n][hid] receives the per-plane sums of d (overwritten: each output tile's sums go to the
+ * workspace, [n][hid][tile], and one ordered reduce makes pool). w1p == NULL is the ratio-1 form
  * (mobilenetv2.py:103-116): hid == cin, k == 3, and up == 2 applies DecoderBlock's nearest
  * Upsample (models.py:264-266) to x first. x2 != NULL feeds channels [c1, cin) from a second
- * tensor (the torch.cat before ada_out, models.py:335). */
+ * tensor (the torch.cat before ada_out, models.py:335). workspace: the floats returned by
+ * ast_mb_expand_dw_workspace_floats for the same arguments (has_x2 = x2 != NULL,
+ * expand = w1p != NULL); <= 0 means the shape is unsupported. */
+long long ast_mb_expand_dw_workspace_floats(int dtype, int has_x2, int c1, int n, int cin, int h, int w, int up,
+                                            int expand, int hid, int cin_pad, int k, int stride, int ho, int wo);
 int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, int cin, int h, int w,
                      int up, const void* w1p, const float* b1, int hid, int cin_pad,
                      const float* wdw, const float* bdw, int k, int stride, void* d, float* pool,
-                     int ho, int wo, void* stream);
+                     int ho, int wo, float* workspace, long long workspace_floats, void* stream);
 
 /* SELayer (mobilenetv2.py:63-81) on the pooled sums (mean = pool / hw), folded into the pw-linear
  * weights w2 [cout][hid]: wg[n][co][c] = w2[co][c] * gate[n][c], written as dtype
@@ -338,14 +363,19 @@ int ast_adaattn_fwd(int dtype, const void* content, const void* style, const flo
                     void* stream);
 
 /* ---------------------------------------------------------------------------------------------
- * Remaining train.py loss terms (SURVEY §8f "next" #2). Scalars are accumulated (atomicAdd) into
- * *loss, which the caller zeroes; gscale (device scalar, may be NULL = 1) scales gradients.
+ * Remaining train.py loss terms (SURVEY §8f "next" #2). Scalars are added into the loss
+ * accumulator `loss` (AST_LOSS_ACC_FLOATS floats, zeroed once by the caller); gscale (device
+ * scalar, may be NULL = 1) scales gradients.
  * ------------------------------------------------------------------------------------------ */
 
 /* SingleDimHistLayer (losses.py:40-57): hist[b][k] = inv_norm * sum_i phi_k(x[b][i]) over the
- * m = C*H*W values of image b, K = 256 bins, L = 1/256, W = L/2.5 (inv_norm = 1/(C*H): the
- * reference divides by x.size(1)*x.size(2)). hist [n][256] is overwritten. */
-int ast_soft_hist_f32(const float* x, int n, long long m, float inv_norm, float* hist, void* stream);
+ * m = C*H*W values of image b (m < 2^30), K = 256 bins, L = 1/256, W = L/2.5 (inv_norm = 1/(C*H):
+ * the reference divides by x.size(1)*x.size(2)). hist [n][256] is overwritten. The bin sums are
+ * exact 32.32 fixed-point integers (order-independent), kept in the workspace of
+ * ast_soft_hist_workspace_floats(n) floats. */
+long long ast_soft_hist_workspace_floats(int n);
+int ast_soft_hist_f32(const float* x, int n, long long m, float inv_norm, float* hist, float* workspace,
+                      long long workspace_floats, void* stream);
 
 /* EarthMoversDistanceLoss (losses.py:8-22) of two histograms [n][256], mean over n
  * (compute_hist_loss, losses.py:84-87): *loss += weight * mean_b sum_t (cdf_x - cdf_y)^2;
@@ -380,7 +410,8 @@ int ast_aug_to_tensor(const unsigned char* src, int h, int w, int cs, float* dst
 int ast_aug_remap_f32(const float* src, int c, int hi, int wi, float* dst, int ho, int wo,
                       const int* coef, void* stream);
 
-/* *acc = sum over pixels of rgb_to_grayscale(img) (zeroed here; adjust_contrast's mean * h*w). */
+/* acc[0] = sum over pixels of rgb_to_grayscale(img) (adjust_contrast's mean * h*w); acc is a loss
+ * accumulator (AST_LOSS_ACC_FLOATS floats, zeroed once by the caller; [0] is overwritten here). */
 int ast_aug_gray_sum_f32(const float* img, int h, int w, float* acc, void* stream);
 
 /* ColorJitter's adjustments and RandomGrayscale on a 3-channel image: op 0 brightness, 1 contrast
@@ -414,18 +445,22 @@ int ast_unpack_images_f32(const float* yp, int n, int c, int h, int w, int G, in
                           float* out, void* stream);
 
 /* C[b][m][n] (+)= sum_k A[b][m][k] B[b][k][n] with element strides (1x1 convs and their grads).
- * ksplit > 1 splits K across workgroups; partial sums are then atomically added (as when C is
- * shared across the batch, sCb == 0): C must hold the starting value (zero it to overwrite).
+ * ksplit > 1 splits K across workgroups, and sCb == 0 with batch > 1 shares C across the batch:
+ * then every (image, K-split) tile goes to the workspace (ast_mbt_gemm_workspace_floats floats,
+ * 0 when neither applies) and one ordered reduce writes / adds C.
  * foldN = P > 0 (batch 1, B n-contiguous): column n is pixel n % P of image n / P, reached through
  * the image strides sBb / sCb; foldK = P > 0 (batch 1, A and B k-contiguous): the same for K. */
+long long ast_mbt_gemm_workspace_floats(int M, int N, int batch, int ksplit, long long sCb);
 int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int K, int batch,
                      long long sAb, long long sAm, long long sAk, long long sBb, long long sBk,
                      long long sBn, long long sCb, long long sCm, long long sCn, int ksplit,
-                     int accumulate, int atomic, int foldK, int foldN, void* stream);
+                     int accumulate, int foldK, int foldN, float* workspace, long long workspace_floats,
+                     void* stream);
 
 /* Depthwise k x k conv (k 3|5, stride 1|2, reflect pad (k-1)/2; mobilenetv2.py:148-149, :116-117):
- * mode 0 out = conv(x, w); 1 out = dx from g (overwritten; needs workspace of
- * ast_mbt_dw_workspace_floats floats: the padded-input gradient); 2 out = dw [c][k*k] from x, g. */
+ * mode 0 out = conv(x, w); 1 out = dx from g (overwritten; the workspace holds the padded-input
+ * gradient); 2 out = dw [c][k*k] from x, g (overwritten; the workspace holds the per-segment
+ * partials). Modes 1 and 2 need ast_mbt_dw_workspace_floats floats of workspace. */
 long long ast_mbt_dw_workspace_floats(int n, int c, int h, int wd, int k);
 int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, float* out, int n,
                    int c, int h, int wd, int k, int s, float* workspace, long long workspace_floats,
@@ -475,13 +510,15 @@ int ast_mbt_plane_f32(int op, const float* x, const float* y, const float* gate,
                       float* out, long long planes, long long hw, void* stream);
 
 /* SELayer MLP (mobilenetv2.py:63-81): hid = relu(W1 pool + b1), z = W2 hid + b2, gate = clamp(z,0,1);
- * backward from dgate: parameter gradients (overwritten) and dpool / hw. */
+ * backward from dgate: parameter gradients (overwritten, summed over images in image order) and
+ * dpool / hw; workspace n * (c + red) floats (the per-image dz, dh). */
 int ast_mbt_se_fc_fwd_f32(const float* pool, const float* w1, const float* b1, const float* w2,
                           const float* b2, int n, int c, int red, float* hid, float* z, float* gate,
                           void* stream);
 int ast_mbt_se_fc_bwd_f32(const float* dgate, const float* z, const float* hid, const float* pool,
                           const float* w1, const float* w2, int n, int c, int red, long long hw,
-                          float* dw1, float* db1, float* dw2, float* db2, float* dpool, void* stream);
+                          float* dw1, float* db1, float* dw2, float* db2, float* dpool, float* workspace,
+                          long long workspace_floats, void* stream);
 
 #ifdef __cplusplus
 }

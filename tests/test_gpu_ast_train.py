@@ -130,13 +130,13 @@ def test_ast_trainer_step_golden(hip_device):
     assert worst <= 1.0, sorted(rows)[-3:]
     assert mean_ratio <= 1.0, mean_ratio
     assert far <= 1e-4 * total, (far, total)
-    # running statistics: rel_inf <= max(1e-4, 3 x the reference's own spread), and on average within
+    # running statistics: rel_inf <= max(1e-4, 2 x the reference's own spread), and on average within
     # the spread itself -- the deep encoder blocks' statistics come from the train-mode pass over the
-    # stylised image (train.py:229); the spread is one 1e-6-perturbation sample, and a run on another
-    # box (different atomic orders in the GPU's reductions) measured one buffer at 2.15 x its spread
+    # stylised image (train.py:229); the spread is one 1e-6-perturbation sample. Every GPU reduction
+    # is in a fixed order (no atomics), so this bound is the same on every run and box.
     bufs = [(rel_inf(b, g[f"buf:{n}"]), float(g[f"bufspread:{n}"]), n)
             for n, b in tr.ast.named_buffers() if f"buf:{n}" in g.files]
-    brows = sorted((e / max(1e-4, 3 * s), n) for e, s, n in bufs)
+    brows = sorted((e / max(1e-4, 2 * s), n) for e, s, n in bufs)
     assert float(np.mean([e / max(1e-4, s) for e, s, _ in bufs])) <= 1.0
     print(f"BN running statistics: {len(brows)} buffers, worst err/bound {brows[-1]}")
     if os.environ.get("AST_GRAD_TABLE"):
