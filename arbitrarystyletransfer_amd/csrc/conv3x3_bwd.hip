@@ -567,10 +567,12 @@ typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
+// as split3 in conv3x3_igemm.hip (finite overflow of hi clamped; non-finite x carried by hi alone)
 __device__ __forceinline__ void wg_split3(float x, bf16_t& hi, bf16_t& mid, bf16_t& lo) {
+  const bool finite = fabsf(x) <= 3.402823466e38f;
   hi = (bf16_t)x;
-  float r = x - (float)hi;
-  if (!(fabsf(x) <= 3.402823466e38f)) r = 0.f;
+  if (finite && !(fabsf((float)hi) <= 3.402823466e38f)) hi = (bf16_t)copysignf(3.38953139e38f, x);
+  float r = finite ? x - (float)hi : 0.f;
   mid = (bf16_t)r;
   lo = (bf16_t)(r - (float)mid);
 }

@@ -472,10 +472,16 @@ __host__ __device__ constexpr int64_t x3_split_offset(int cin, int cout) {  // f
   return (int64_t)((cin + 7) / 8 * 8) * 9 * ((cout + 63) / 64 * 64);
 }
 
+// x = hi + mid + lo exactly for finite x. A finite |x| above bf16's largest value (3.3895e38) would
+// round hi to inf: hi is clamped to that largest value instead, and the remainder stays exact.
+// Non-finite x: hi = x, mid = lo = 0. The MFMA also multiplies hi by the weight's mid and lo terms,
+// which are often exactly 0, so an inf input gives NaN outputs where torch's inf * w gives +-inf
+// (NaN inputs give NaN, as in torch); tests/test_gpu_parity.py pins both behaviours.
 __device__ __forceinline__ void split3(float x, bf16& hi, bf16& mid, bf16& lo) {
+  const bool finite = fabsf(x) <= 3.402823466e38f;
   hi = (bf16)x;
-  float r = x - (float)hi;
-  if (!(fabsf(x) <= 3.402823466e38f)) r = 0.f;  // inf / NaN: carried by hi alone (torch's inf*w)
+  if (finite && !(fabsf((float)hi) <= 3.402823466e38f)) hi = (bf16)copysignf(3.38953139e38f, x);
+  float r = finite ? x - (float)hi : 0.f;
   mid = (bf16)r;
   lo = (bf16)(r - (float)mid);
 }

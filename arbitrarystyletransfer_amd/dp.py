@@ -1,6 +1,10 @@
 """Data parallelism for the training step (BASELINE.json config 4): one process per GPU,
-batch-sharded, gradients averaged by a single all-reduce over xGMI (torch.distributed "nccl" =
+batch-sharded, gradients reduced by a single all-reduce over xGMI (torch.distributed "nccl" =
 RCCL on ROCm).
+
+Whenever a default process group is initialised the trainers take this path, at any world size:
+a world of 1 runs the same collectives (trivial on one rank), which is how the RCCL branches are
+exercised on a one-GPU box (tests/test_gpu_rccl.py).
 
 The trainable parameters' gradients live in one flat fp32 arena: the HIP weight-gradient kernel
 writes each dW/db straight into its slice (functional.GRAD_ARENA), autograd adopts those views as
@@ -35,6 +39,21 @@ def shard_weight(global_batch: int, rank: int, world: int) -> float:
     return (b - a) / global_batch
 
 
+def active() -> bool:
+    """True when a default process group is initialised (the data-parallel path is taken)."""
+    return dist.is_available() and dist.is_initialized()
+
+
+def is_main() -> bool:
+    """Rank 0, or no process group: the process that writes checkpoints and logs."""
+    return not active() or dist.get_rank() == 0
+
+
+def barrier() -> None:
+    if active():
+        dist.barrier()
+
+
 def init_from_env(backend=None, device=None):
     """Initialise the default process group from torchrun's env (RANK/WORLD_SIZE/MASTER_*)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -50,7 +69,9 @@ def init_from_env(backend=None, device=None):
 
 class FlatGradArena:
     """One contiguous gradient buffer for `params`; registers each parameter's slice so the
-    backward kernels write into it, and averages it across ranks in one all-reduce."""
+    backward kernels write into it, and reduces it across ranks in one all-reduce: a SUM for the
+    trainers (each rank's loss terms already carry their shard weight, so the sum is the
+    full-batch gradient, uneven shards included), or an AVG (average=True, DDP semantics)."""
 
     def __init__(self, params, device=None, average=True):
         self.params = list(params)
@@ -102,7 +123,7 @@ class FlatGradArena:
             if p.grad is not None and p.grad.data_ptr() != self.view_for(p).data_ptr():
                 self.view_for(p).copy_(p.grad)
                 p.grad = self.view_for(p)
-        if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        if not active():
             return
         if dist.get_backend(group) == "nccl":
             dist.all_reduce(self.flat, op=dist.ReduceOp.AVG if self.average else dist.ReduceOp.SUM, group=group)
@@ -132,7 +153,8 @@ def broadcast_style_stats(style_mean, style_std, src: int = 0, group=None):
 # mode), so a batch-sharded step must merge the statistics over ranks. Forward: every rank's
 # per-channel (count, mean, M2) in double, [c][3], is all-gathered (W*c*24 bytes) and merged on
 # device (Chan's update); backward: the per-channel sums (dy, dy*xhat) are all-reduced for the
-# input gradient, while dgamma/dbeta stay local (the gradient all-reduce averages them, as DDP).
+# input gradient, while dgamma/dbeta stay local: each rank's are the gradient of its own
+# shard-weighted loss, and the gradient all-reduce SUMS them into the full-batch gradient.
 # ------------------------------------------------------------------------------------------------
 def convert_sync_batchnorm(module: torch.nn.Module, group=None) -> torch.nn.Module:
     """Mark every BatchNorm2d of `module` for cross-rank statistics (mbtrain.BatchNormTrainFn);
@@ -145,11 +167,10 @@ def convert_sync_batchnorm(module: torch.nn.Module, group=None) -> torch.nn.Modu
 
 
 def sync_group(bn):
-    """The process group a BatchNorm syncs over, or None (not marked / not distributed / W = 1)."""
-    if not getattr(bn, "_ast_sync", False) or not dist.is_available() or not dist.is_initialized():
+    """The process group a BatchNorm syncs over, or None (not marked / not distributed)."""
+    if not getattr(bn, "_ast_sync", False) or not active():
         return None
-    group = getattr(bn, "_ast_sync_group", None)
-    return None if dist.get_world_size(group) == 1 else (group or dist.group.WORLD)
+    return getattr(bn, "_ast_sync_group", None) or dist.group.WORLD
 
 
 def _staged(t, group):
@@ -167,6 +188,18 @@ def all_gather_bn_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
     else:
         dist.all_gather(list(out.unbind(0)), src, group=group)
     return out.to(stats.device)
+
+
+def global_terms(terms: dict, weights: dict, group=None) -> dict:
+    """Full-batch values of per-rank loss terms, for logging: sum over ranks of weight * term (the
+    shard weight for batch-mean terms, 1 for batch-sum terms such as tv). One all-reduce of a
+    small stacked vector; in a single process the terms come back unchanged."""
+    keys = sorted(terms)
+    if not active():
+        return {k: terms[k] for k in keys}
+    vec = torch.stack([terms[k].detach().float().reshape(()) * weights.get(k, 1.0) for k in keys])
+    all_reduce_sum(vec, group)
+    return {k: vec[i] for i, k in enumerate(keys)}
 
 
 def all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:

@@ -81,7 +81,7 @@ class AdaINTrainer:
         self.grad_hook = grad_hook  # called between backward and the optimizer step
         self.rank, self.world = 0, 1
         self.grad_arena = None
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if dp.active():   # any world size: a world of 1 runs the same collectives
             self.rank, self.world = dist.get_rank(), dist.get_world_size()
             dp.shard_range(self.args.batch_size, self.rank, self.world)   # raises on an empty shard
             self.grad_arena = dp.FlatGradArena(self.params, average=False)
@@ -159,17 +159,23 @@ class AdaINTrainer:
         self.optim.step()
         out["grad_norm"] = self.optim.last_grad_norm
         if record:  # device -> host syncs, as train.py:302-306 does every step
+            keys = ("content_loss", "style_loss", "lf_loss", "tv_loss") + (("org_img_loss",) if "org_img_loss" in out else ())
+            vals = dp.global_terms({k: out[k] for k in keys}, {k: w for k in keys if k != "tv_loss"})
             for k in ("content_loss", "style_loss", "lf_loss", "tv_loss"):
-                self.train_dict[k].append(float(out[k].item()))
-            self.train_dict["org_img_loss"].append(float(out["org_img_loss"].item()) if "org_img_loss" in out else 0.0)
+                self.train_dict[k].append(float(vals[k].item()))
+            self.train_dict["org_img_loss"].append(float(vals["org_img_loss"].item()) if "org_img_loss" in vals else 0.0)
         return out
 
     # ---- checkpoints (train.py:103-133) -------------------------------------------------------
     def save(self):
-        os.makedirs(self.args.save_dir, exist_ok=True)
-        torch.save({"ast": self.net.state_dict(), "ast_optim": self.optim.state_dict()}, self.save_file)
-        with open(self.train_dict_file, "w") as f:
-            json.dump(self.train_dict, f)
+        """Rank 0 writes (every rank holds the same parameters after the reduced step); the others
+        wait at a barrier so no rank reads a half-written file."""
+        if dp.is_main():
+            os.makedirs(self.args.save_dir, exist_ok=True)
+            torch.save({"ast": self.net.state_dict(), "ast_optim": self.optim.state_dict()}, self.save_file)
+            with open(self.train_dict_file, "w") as f:
+                json.dump(self.train_dict, f)
+        dp.barrier()
 
     def load(self):
         d = torch.load(self.save_file, map_location=self.device, weights_only=True)
@@ -224,7 +230,7 @@ class ASTTrainer:
         self.grad_hook = grad_hook
         self.rank, self.world = 0, 1
         self.grad_arena = None
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if dp.active():   # any world size: a world of 1 runs the same collectives
             self.rank, self.world = dist.get_rank(), dist.get_world_size()
             dp.shard_range(self.args.batch_size, self.rank, self.world)
             dp.convert_sync_batchnorm(self.ast)
@@ -295,8 +301,11 @@ class ASTTrainer:
         self.ast_optim.step()                                                           # :292, :300
         out["grad_norm"] = self.ast_optim.last_grad_norm
         if record:                                                                      # :302-306
-            for k in ("content_loss", "style_loss", "lf_loss", "tv_loss", "org_img_loss"):
-                self.train_dict[k].append(float(out[k].item()))
+            keys = ("content_loss", "style_loss", "lf_loss", "tv_loss", "org_img_loss")
+            w = 1.0 if self.world == 1 else dp.shard_weight(self.args.batch_size, self.rank, self.world)
+            vals = dp.global_terms({k: out[k] for k in keys}, {k: w for k in keys if k != "tv_loss"})
+            for k in keys:
+                self.train_dict[k].append(float(vals[k].item()))
         return out
 
     def train(self):
@@ -307,10 +316,12 @@ class ASTTrainer:
                 self.save()
 
     def save(self):
-        os.makedirs(self.args.save_dir, exist_ok=True)
-        torch.save({"ast": self.ast.state_dict(), "ast_optim": self.ast_optim.state_dict()}, self.save_file)
-        with open(self.train_dict_file, "w") as f:
-            json.dump(self.train_dict, f)
+        if dp.is_main():   # rank 0 writes, the others wait (identical parameters after the reduced step)
+            os.makedirs(self.args.save_dir, exist_ok=True)
+            torch.save({"ast": self.ast.state_dict(), "ast_optim": self.ast_optim.state_dict()}, self.save_file)
+            with open(self.train_dict_file, "w") as f:
+                json.dump(self.train_dict, f)
+        dp.barrier()
 
     def load(self):
         d = torch.load(self.save_file, map_location=self.device, weights_only=True)
@@ -357,7 +368,7 @@ class AutoencoderTrainer:
         # shards included)
         self.grad_arena = None
         self.rank, self.world = 0, 1
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if dp.active():   # any world size: a world of 1 runs the same collectives
             self.rank, self.world = dist.get_rank(), dist.get_world_size()
             dp.shard_range(self.args.batch_size, self.rank, self.world)   # raises on an empty shard
             dp.convert_sync_batchnorm(self.model)
@@ -392,9 +403,12 @@ class AutoencoderTrainer:
             self.grad_arena.all_reduce()
         self.ae_optim.step()                                                           # clip 10 + Adam, :159-165
         out["grad_norm"] = self.ae_optim.last_grad_norm
-        if record:
-            self.train_dict["train_loss"].append(float(out["recon_loss"].item()))
-            self.train_dict["perp_loss"].append(float(out["content_loss"].item()))
+        if record:   # full-batch values (shard-weighted sums over ranks)
+            w = 1.0 if self.world == 1 else dp.shard_weight(self.args.batch_size, self.rank, self.world)
+            vals = dp.global_terms({"recon_loss": out["recon_loss"], "content_loss": out["content_loss"]},
+                                   {"recon_loss": w, "content_loss": w})
+            self.train_dict["train_loss"].append(float(vals["recon_loss"].item()))
+            self.train_dict["perp_loss"].append(float(vals["content_loss"].item()))
         return out
 
     def train(self):
@@ -415,10 +429,12 @@ class AutoencoderTrainer:
         self.model.train()
 
     def save(self):
-        os.makedirs(self.args.save_dir, exist_ok=True)
-        torch.save({"AE": self.model.state_dict(), "optim": self.ae_optim.state_dict()}, self.save_file)
-        with open(self.train_dict_file, "w") as f:
-            json.dump(self.train_dict, f)
+        if dp.is_main():   # rank 0 writes, the others wait (identical parameters after the reduced step)
+            os.makedirs(self.args.save_dir, exist_ok=True)
+            torch.save({"AE": self.model.state_dict(), "optim": self.ae_optim.state_dict()}, self.save_file)
+            with open(self.train_dict_file, "w") as f:
+                json.dump(self.train_dict, f)
+        dp.barrier()
 
     def load(self):
         d = torch.load(self.save_file, map_location=self.device, weights_only=True)

@@ -163,3 +163,50 @@ def test_ast_trainer_checkpoint_roundtrip(tmp_path, hip_device):
     for (k, v), (k2, v2) in zip(tr.ast.state_dict().items(), tr2.ast.state_dict().items()):
         assert k == k2 and torch.equal(v, v2), k
     assert tr2.train_dict == tr.train_dict and len(tr2.train_dict["lf_loss"]) == 1
+
+
+def test_ast_trainer_dp_uneven_matches_single_process(tmp_path, hip_device):
+    """ASTTrainer's data-parallel path: 2 ranks over gloo with an uneven 2 + 1 shard of
+    a global batch of 3 -- SyncBatchNorm over the train-mode encoder, shard-weighted loss terms,
+    one SUM all-reduce of the gradient arena -- against the single-process B = 3 step: reduced
+    gradients, updated parameters, BN running statistics, the logged (global) loss.
+    The two sides differ only in fp32 summation order (BN statistics merged per rank, gradient
+    partial sums per shard), which the train-mode step amplifies through ReLU / max-pool routing
+    (the golden fixture's 1e-6-perturbation spread reaches 4% on single tensors): bounds are a
+    median per-tensor error of 1e-4 and a worst of 2e-2 of max|g|."""
+    import socket
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import ast_dp_worker as W
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    out = str(tmp_path / "dp.npz")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", W.__file__, out],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    got = np.load(out)
+    snap = {}
+    tr = W.make_trainer(hip_device, lambda ps: snap.update({n: p.grad.detach().clone()
+                                                            for n, p in tr.ast.named_parameters()}))
+    content, style = W.inputs()
+    o = tr.train_step(content.to(hip_device), style.to(hip_device), record=True)
+    np.testing.assert_allclose(float(got["grad_norm"]), float(o["grad_norm"]), rtol=1e-3)
+    np.testing.assert_allclose(float(got["content_loss_logged"]), tr.train_dict["content_loss"][-1], rtol=1e-5)
+    errs = []
+    for n, p in tr.ast.named_parameters():
+        ref = snap[n].cpu().numpy()
+        e = float(np.abs(got[f"grad:{n}"] - ref).max()) / max(float(np.abs(ref).max()), 1e-5 * float(o["grad_norm"]))
+        errs.append((e, n))
+        d = np.abs(got[f"param:{n}"] - p.detach().cpu().numpy())
+        assert d.max() <= 2.05 * 2e-4, n   # Adam's first step moves each parameter by at most ~lr
+    errs.sort()
+    med = errs[len(errs) // 2][0]
+    print(f"AST DP (2 + 1 shards) vs single process: median grad err {med:.2e}, worst {errs[-1]}")
+    assert med <= 1e-4 and errs[-1][0] <= 2e-2, errs[-3:]
+    for n, b in tr.ast.named_buffers():
+        if b.is_floating_point():
+            assert rel_inf(got[f"buf:{n}"], b) <= 1e-4, n

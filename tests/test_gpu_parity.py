@@ -120,6 +120,33 @@ def test_conv3x3_nan_propagates(hip_device):
         np.testing.assert_array_equal(np.isnan(g), np.isnan(r))
 
 
+def test_conv3x3_split_bf16_nonfinite_and_overflow(hip_device):
+    """The split-bf16 kernel's contract for extreme inputs (csrc/conv3x3_igemm.hip split3):
+    * a finite input above bf16's largest value (3.3895e38) is split exactly (hi clamped), so a
+      single large pixel gives the same output as torch, to fp32 accuracy;
+    * an inf input gives NaN at every output it reaches (torch gives +-inf there: the MFMA also
+      multiplies hi = inf by the weight's mid / lo terms, which are often 0), all other outputs
+      unchanged; a NaN input gives NaN exactly where torch does."""
+    n, cin, h, w, cout = 1, 64, 16, 32, 64
+    wt = torch.from_numpy(synth.conv_weight(41, cout, cin, 3)) * 0.01
+    wp = ops.pack_conv3x3(wt.to(hip_device))
+    x = torch.zeros(n, cin, h, w)
+    x[0, 7, 5, 9] = 3.4e38
+    ref, _, _ = oracle_conv(x.double(), wt.double(), None, 1, "zeros", False, False)
+    got, _, _ = ops.conv3x3(x.to(hip_device), wp, None, cout, want_pre=True, want_act=False)
+    assert torch.isfinite(got).all()
+    assert rel_inf(got, ref.float()) <= 2e-6
+    x = torch.from_numpy(synth.image(42, (n, cin, h, w)))
+    x[0, 7, 5, 9] = float("inf")
+    ref, _, _ = oracle_conv(x, wt, None, 1, "zeros", False, False)
+    got, _, _ = ops.conv3x3(x.to(hip_device), wp, None, cout, want_pre=True, want_act=False)
+    g, r = got.cpu().numpy(), ref.numpy()
+    touched = ~np.isfinite(r)
+    assert touched.sum() == cout * 9
+    assert np.isnan(g[touched]).all()
+    assert np.allclose(g[~touched], r[~touched], rtol=1e-5, atol=1e-5 * np.abs(r[~touched]).max())
+
+
 def test_adain_golden(golden, hip_device):
     g = golden("adain_kat")
     c, s = T(g["content"], hip_device), T(g["style"], hip_device)
