@@ -104,6 +104,7 @@ def test_dw_and_se_backward(k, s, hip_device):
     g = rnd(9, (3, 24, (33 - 1) // s + 1, (40 - 1) // s + 1), hip_device, 2.0, -1.0)
 
     def step():
+        blk.zero_grad(set_to_none=True)
         xi = x.clone().requires_grad_()
         y = blk(xi)
         y.backward(g)
