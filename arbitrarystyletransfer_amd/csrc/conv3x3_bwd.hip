@@ -307,7 +307,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgArgs a) {
       }
     }
   }
-  if (a.db && cig == 0 && co0 + (tid & 63) < a.Cout) a.db[split * a.Cout + co0 + (tid & 63)] = bacc;
+  if (a.db && cig == 0) {  // the 4 quarter-partials of each co, added in quarter order
+    __shared__ float bq[4][64];
+    __syncthreads();
+    bq[tid >> 6][tid & 63] = bacc;
+    __syncthreads();
+    if (tid < 64 && co0 + tid < a.Cout) a.db[split * a.Cout + co0 + tid] = (bq[0][tid] + bq[1][tid]) + (bq[2][tid] + bq[3][tid]);
+  }
 }
 
 // Weight gradient for Cout <= 4 (the decoders' image convs, models.py:627), or Cout <= 16 with
@@ -544,7 +550,13 @@ __global__ __launch_bounds__(256, 2) void wgrad2_kernel(WgArgs a) {
       const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
       dwp[((int64_t)co * a.Cin + ci) * 9 + t] = acc[t][r];
     }
-  if (a.db && cig == 0) a.db[(int64_t)split * a.Cout + co0 + (tid & 63)] = bacc;
+  if (a.db && cig == 0) {  // the 4 quarter-partials of each co, added in quarter order
+    __shared__ float bq[4][64];
+    __syncthreads();
+    bq[tid >> 6][tid & 63] = bacc;
+    __syncthreads();
+    if (tid < 64) a.db[(int64_t)split * a.Cout + co0 + tid] = (bq[0][tid] + bq[1][tid]) + (bq[2][tid] + bq[3][tid]);
+  }
 #undef WG2_ITEM
 #undef WG2_HALO
 }

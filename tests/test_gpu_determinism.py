@@ -68,10 +68,19 @@ WGRAD_CASES = [
 
 @pytest.mark.parametrize("case", WGRAD_CASES)
 def test_conv_wgrad(case, hip_device):
+    """Bitwise run to run, and equal to torch's CPU weight / bias gradient (rel_inf 1e-5)."""
     n, cin, h, w, cout, up, pad = case
     x = rnd(2, (n, cin, h, w), hip_device)
     dy = rnd(3, (n, cout, h * up, w * up), hip_device, 2.0, -1.0)
-    twice(lambda: Fn.conv_weight_grad(x, dy, cout, up, pad))
+    dw, db = twice(lambda: Fn.conv_weight_grad(x, dy, cout, up, pad))
+    xc = x.double().cpu()
+    if up == 2:
+        xc = torch.nn.functional.interpolate(xc, scale_factor=2, mode="nearest")
+    xc = torch.nn.functional.pad(xc, (1, 1, 1, 1), mode="reflect" if pad == "reflect" else "constant")
+    ref = torch.nn.grad.conv2d_weight(xc, (cout, cin, 3, 3), dy.double().cpu())
+    for got, want in ((dw, ref), (db, dy.double().cpu().sum(dim=(0, 2, 3)))):
+        err = float((got.double().cpu() - want).abs().max() / want.abs().max())
+        assert err <= 1e-5, err
 
 
 def test_mbt_gemm_ksplit_and_shared(hip_device):
