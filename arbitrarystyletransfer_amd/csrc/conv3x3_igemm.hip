@@ -475,8 +475,8 @@ __host__ __device__ constexpr int64_t x3_split_offset(int cin, int cout) {  // f
 // x = hi + mid + lo exactly for finite x. A finite |x| above bf16's largest value (3.3895e38) would
 // round hi to inf: hi is clamped to that largest value instead, and the remainder stays exact.
 // Non-finite x: hi = x, mid = lo = 0. The MFMA also multiplies hi by the weight's mid and lo terms,
-// which are often exactly 0, so an inf input gives NaN outputs where torch's inf * w gives +-inf
-// (NaN inputs give NaN, as in torch); tests/test_gpu_parity.py pins both behaviours.
+// which are often exactly 0, so an output reached by an inf input is +-inf (as torch's inf * w) or
+// NaN; NaN inputs give NaN, as in torch. tests/test_gpu_parity.py pins both behaviours.
 __device__ __forceinline__ void split3(float x, bf16& hi, bf16& mid, bf16& lo) {
   const bool finite = fabsf(x) <= 3.402823466e38f;
   hi = (bf16)x;

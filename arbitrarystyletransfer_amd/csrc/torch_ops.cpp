@@ -9,7 +9,7 @@
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 
 #include <tuple>
 
@@ -58,7 +58,7 @@ at::Tensor adain(const at::Tensor& content_, const at::Tensor& style_, double al
                   content.size(1) == style.size(1),
               "AdaIN needs NCHW maps with equal (N, C): ", content.sizes(), " vs ", style.sizes());
   same_device(content, style, "style_map");
-  const c10::hip::HIPGuard guard(content.device());
+  const c10::DeviceGuard guard(content.device());
   at::Tensor out = at::empty_like(content);
   AST_CALL("adain", ast_adain_f32(content.data_ptr<float>(), style.data_ptr<float>(), out.data_ptr<float>(),
                                   (int)content.size(0), (int)content.size(1), (int)content.size(2),
@@ -78,7 +78,7 @@ at::Tensor adain_meta(const at::Tensor& content, const at::Tensor& style, double
 std::tuple<at::Tensor, at::Tensor> channel_stats(const at::Tensor& x_, bool unbiased, double eps) {
   at::Tensor x = dev_f32(x_, "x");
   TORCH_CHECK(x.dim() == 4, "channel_stats expects NCHW, got ", x.sizes());
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   at::Tensor mean = at::empty({x.size(0), x.size(1), 1, 1}, x.options());
   at::Tensor std_ = at::empty_like(mean);
   AST_CALL("channel_stats", ast_channel_stats_f32(x.data_ptr<float>(), mean.data_ptr<float>(), std_.data_ptr<float>(),
@@ -99,7 +99,7 @@ at::Tensor conv3x3_pack(const at::Tensor& w_) {
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "conv3x3 weight must be [cout, cin, 3, 3], got ",
               w.sizes());
   const int cout = (int)w.size(0), cin = (int)w.size(1);
-  const c10::hip::HIPGuard guard(w.device());
+  const c10::DeviceGuard guard(w.device());
   at::Tensor out = at::empty({(int64_t)ast_conv3x3_packed_numel(cout, cin)}, w.options());
   AST_CALL("conv3x3_pack", ast_conv3x3_pack_weights_f32(w.data_ptr<float>(), out.data_ptr<float>(), cout, cin,
                                                         cur_stream(w)));
@@ -151,7 +151,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> conv3x3_fwd(
     same_device(x, *in_std, "in_std");
     TORCH_CHECK(in_mean->numel() == s.cin && in_std->numel() == s.cin, "normalisation stats must have cin entries");
   }
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   auto mk = [&](bool want, int64_t h, int64_t w) {
     return want ? at::empty({s.n, cout, h, w}, x.options()) : at::empty({0}, x.options());
   };
@@ -181,7 +181,7 @@ at::Tensor gram(const at::Tensor& f_) {
   at::Tensor f = dev_f32(f_, "tensor");
   TORCH_CHECK(f.dim() == 4, "gram_matrix expects [B, C, H, W], got ", f.sizes());
   const int64_t b = f.size(0), c = f.size(1), hw = f.size(2) * f.size(3);
-  const c10::hip::HIPGuard guard(f.device());
+  const c10::DeviceGuard guard(f.device());
   at::Tensor g = at::empty({b, c, c}, f.options());
   const long long wsf = ast_gram_workspace_floats((int)b, (int)c, hw);
   at::Tensor ws = at::empty({wsf > 0 ? wsf : 1}, f.options());

@@ -24,10 +24,17 @@ def inputs():
     return c, s
 
 
+ATT_SCALE = 0.125   # as test_ast_trainer_step_golden: W_q, W_k scaled after the live init (diffuse attention)
+
+
 def make_trainer(device, hook):
     torch.manual_seed(0)
-    return ASTTrainer(default_ast_args(batch_size=GLOBAL_BATCH), device=device,
-                      ast=models.AST(attention=True).load_live_init(), grad_hook=hook)
+    ast = models.AST(attention=True).load_live_init()
+    with torch.no_grad():
+        for att in (ast.ada_att_1, ast.ada_att_2):
+            att.W_q.weight.mul_(ATT_SCALE)
+            att.W_k.weight.mul_(ATT_SCALE)
+    return ASTTrainer(default_ast_args(batch_size=GLOBAL_BATCH), device=device, ast=ast, grad_hook=hook)
 
 
 def main(out_path):
