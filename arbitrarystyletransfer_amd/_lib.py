@@ -59,6 +59,7 @@ SIGNATURES = {
     "ast_grad_norm_f32": (_i, [_p, _i, _ll, _p, _f, _p, _p]),
     "ast_grad_scale_f32": (_i, [_p, _i, _ll, _p, _p]),
     "ast_adam_step_f32": (_i, [_p, _i, _ll, _p, _d, _d, _d, _d, _i, _p]),
+    "ast_adam_step_sched_f32": (_i, [_p, _i, _ll, _p, _d, _d, _d, _d, _p, _i, _p]),
     "ast_mb_expand_dw_workspace_floats": (_ll, [_i] * 15),
     "ast_mb_expand_dw": (_i, [_i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p,
                               _i, _i, _p, _ll, _p]),

@@ -534,15 +534,67 @@ __host__ __device__ constexpr int x3_srel(int i, int ky) { return UP == 1 ? i + 
 // writes its accumulators (+bias) to its own LDS region [32 channels][RM rows][32 px + 4], then
 // stores rows: 8 lanes per 128-byte run, pre-ReLU / ReLU / 2x2 max-pool as store_tiles. The
 // caller's barrier must precede it (the region overlaps the operand tiles).
-template <int RM, int RN>
-__device__ __forceinline__ void store_tiles_staged(const ConvArgs& a, const f32x16 (&acc)[RM][RN], int n, int x0,
-                                                   int y0, int row0, int n0c, int h, int l32, int lane,
-                                                   float* __restrict__ region) {
+// Row stores of one 32-channel group from a wave's staged region [32 channels][RM rows][36 floats]
+// (channel ch = output channel cbase + ch): pre-ReLU / ReLU float4 rows, 8 lanes per 128-byte run,
+// and the fused 2x2 max-pool.
+template <int RM>
+__device__ __forceinline__ void store_region(const ConvArgs& a, const float* __restrict__ region, int n, int x0,
+                                             int y0, int row0, int cbase, int lane) {
   constexpr int RP = 36;  // row pitch (floats): 32 px + 4
   const int H = a.H, W = a.W;
   const int64_t plane = (int64_t)H * W;
   const bool vec4 = (W & 3) == 0;
   const int Ho = H >> 1, Wo = W >> 1;
+  if (a.y_pre || a.y_act) {
+#pragma unroll
+    for (int it = 0; it < 32 * RM * 8 / 64; ++it) {
+      const int item = it * 64 + lane;
+      const int q = item & 7, row = (item >> 3) % RM, ch = item / (8 * RM);
+      const int co = cbase + ch, yy = y0 + row0 + row, xx = x0 + 4 * q;
+      if (co >= a.Cout || yy >= H || xx >= W) continue;
+      const float4 v = *reinterpret_cast<const float4*>(region + (ch * RM + row) * RP + 4 * q);
+      const int64_t off = ((int64_t)n * a.Cout + co) * plane + (int64_t)yy * W + xx;
+      const bool full = vec4 && xx + 3 < W;
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      if (a.y_pre) {
+        if (full) *reinterpret_cast<float4*>(a.y_pre + off) = v;
+        else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_pre[off + r] = vv[r];
+      }
+      if (a.y_act) {
+        const float4 u = make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
+        if (full) *reinterpret_cast<float4*>(a.y_act + off) = u;
+        else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_act[off + r] = relu_f(vv[r]);
+      }
+    }
+  }
+  if (a.y_pool) {
+#pragma unroll
+    for (int it = 0; it < 32 * (RM / 2) * 8 / 64; ++it) {
+      const int item = it * 64 + lane;
+      const int q = item & 7, prow = (item >> 3) % (RM / 2), ch = item / (8 * (RM / 2));
+      const int co = cbase + ch, py = (y0 + row0) / 2 + prow, px = (x0 + 4 * q) >> 1;
+      if (co >= a.Cout || py >= Ho || px >= Wo) continue;
+      const float4 r0 = *reinterpret_cast<const float4*>(region + (ch * RM + 2 * prow) * RP + 4 * q);
+      const float4 r1 = *reinterpret_cast<const float4*>(region + (ch * RM + 2 * prow + 1) * RP + 4 * q);
+      const float m0 = max_nan(relu_f(r0.x), relu_f(r1.x)), m1 = max_nan(relu_f(r0.y), relu_f(r1.y));
+      const float m2 = max_nan(relu_f(r0.z), relu_f(r1.z)), m3 = max_nan(relu_f(r0.w), relu_f(r1.w));
+      const float p0 = max_nan(m0, m1), p1 = max_nan(m2, m3);
+      const int64_t off = ((int64_t)n * a.Cout + co) * Ho * Wo + (int64_t)py * Wo + px;
+      if (px + 1 < Wo && (Wo & 1) == 0) {
+        *reinterpret_cast<float2*>(a.y_pool + off) = make_float2(p0, p1);
+      } else {
+        a.y_pool[off] = p0;
+        if (px + 1 < Wo) a.y_pool[off + 1] = p1;
+      }
+    }
+  }
+}
+
+template <int RM, int RN>
+__device__ __forceinline__ void store_tiles_staged(const ConvArgs& a, const f32x16 (&acc)[RM][RN], int n, int x0,
+                                                   int y0, int row0, int n0c, int h, int l32, int lane,
+                                                   float* __restrict__ region) {
+  constexpr int RP = 36;  // row pitch (floats): 32 px + 4
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
     {
@@ -558,49 +610,7 @@ __device__ __forceinline__ void store_tiles_staged(const ConvArgs& a, const f32x
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done
     __builtin_amdgcn_wave_barrier();
-    if (a.y_pre || a.y_act) {
-#pragma unroll
-      for (int it = 0; it < 32 * RM * 8 / 64; ++it) {
-        const int item = it * 64 + lane;
-        const int q = item & 7, row = (item >> 3) % RM, ch = item / (8 * RM);
-        const int co = n0c + j * 32 + ch, yy = y0 + row0 + row, xx = x0 + 4 * q;
-        if (co >= a.Cout || yy >= H || xx >= W) continue;
-        const float4 v = *reinterpret_cast<const float4*>(region + (ch * RM + row) * RP + 4 * q);
-        const int64_t off = ((int64_t)n * a.Cout + co) * plane + (int64_t)yy * W + xx;
-        const bool full = vec4 && xx + 3 < W;
-        const float vv[4] = {v.x, v.y, v.z, v.w};
-        if (a.y_pre) {
-          if (full) *reinterpret_cast<float4*>(a.y_pre + off) = v;
-          else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_pre[off + r] = vv[r];
-        }
-        if (a.y_act) {
-          const float4 u = make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
-          if (full) *reinterpret_cast<float4*>(a.y_act + off) = u;
-          else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_act[off + r] = relu_f(vv[r]);
-        }
-      }
-    }
-    if (a.y_pool) {
-#pragma unroll
-      for (int it = 0; it < 32 * (RM / 2) * 8 / 64; ++it) {
-        const int item = it * 64 + lane;
-        const int q = item & 7, prow = (item >> 3) % (RM / 2), ch = item / (8 * (RM / 2));
-        const int co = n0c + j * 32 + ch, py = (y0 + row0) / 2 + prow, px = (x0 + 4 * q) >> 1;
-        if (co >= a.Cout || py >= Ho || px >= Wo) continue;
-        const float4 r0 = *reinterpret_cast<const float4*>(region + (ch * RM + 2 * prow) * RP + 4 * q);
-        const float4 r1 = *reinterpret_cast<const float4*>(region + (ch * RM + 2 * prow + 1) * RP + 4 * q);
-        const float m0 = max_nan(relu_f(r0.x), relu_f(r1.x)), m1 = max_nan(relu_f(r0.y), relu_f(r1.y));
-        const float m2 = max_nan(relu_f(r0.z), relu_f(r1.z)), m3 = max_nan(relu_f(r0.w), relu_f(r1.w));
-        const float p0 = max_nan(m0, m1), p1 = max_nan(m2, m3);
-        const int64_t off = ((int64_t)n * a.Cout + co) * Ho * Wo + (int64_t)py * Wo + px;
-        if (px + 1 < Wo && (Wo & 1) == 0) {
-          *reinterpret_cast<float2*>(a.y_pool + off) = make_float2(p0, p1);
-        } else {
-          a.y_pool[off] = p0;
-          if (px + 1 < Wo) a.y_pool[off + 1] = p1;
-        }
-      }
-    }
+    store_region<RM>(a, region, n, x0, y0, row0, n0c + j * 32, lane);
     if (j + 1 < RN) {
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();  // reads of this j done before the next j's writes
@@ -608,7 +618,16 @@ __device__ __forceinline__ void store_tiles_staged(const ConvArgs& a, const f32x
   }
 }
 
-template <int WM, int RM, int RN, int UP, int OCC>
+// M16: the same kernel on v_mfma_f32_16x16x32_bf16 (16 pixels x 16 output channels x K 32). The six
+// split products fold into three K-32 MFMAs -- K = (16 channels of one term | 16 of another):
+//   [x_hi | x_mid] . [w_hi ; w_hi]  = x_hi w_hi  + x_mid w_hi
+//   [x_hi | x_lo ] . [w_mid; w_hi]  = x_hi w_mid + x_lo w_hi
+//   [x_hi | x_mid] . [w_lo ; w_mid] = x_hi w_lo  + x_mid w_mid
+// -- the same products and cycles per FLOP as the 32x32x16 form; on random data the chip holds a
+// higher clock with the 16x16 shape (MI355X_MICROARCH.md, DVFS give-back item 7). A lane's k-group
+// g = lane >> 4 selects the term plane (g < 2: the first, else the second) and the 8-channel half
+// (g & 1), so every operand is still one ds_read_b128 from the same LDS images.
+template <int WM, int RM, int RN, int UP, int OCC, bool M16 = false>
 __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   using C = X3Cfg<WM, RM, RN, UP>;
   constexpr int NT = C::NT, TH = C::TH, BN = C::BN, SR = C::SR, SC = C::SC, A_PLANE = C::A_PLANE;
@@ -708,18 +727,39 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
       if (tid + i * NT < C::B_UNITS) Bs[b_dst[i]] = rb[i];                                              \
   }
 
-  f32x16 acc[RM][RN];
+  constexpr int Q = 2 * RN;  // M16: 16-channel column tiles per wave
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  f32x16 acc[M16 ? 1 : RM][M16 ? 1 : RN];
+  f32x4v acc16[M16 ? RM : 1][M16 ? 2 : 1][M16 ? Q : 1];
+  if constexpr (M16) {
 #pragma unroll
-  for (int i = 0; i < RM; ++i)
+    for (int i = 0; i < RM; ++i)
 #pragma unroll
-    for (int j = 0; j < RN; ++j)
+      for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int q = 0; q < Q; ++q) acc16[i][pt][q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  }
 
   int acol[3];
 #pragma unroll
   for (int kx = 0; kx < 3; ++kx) acol[kx] = ((x0 + l32 + kx - 1) >> (UP - 1)) - sx0 + 1;
   const int srow0 = wm * RM / UP;
+  // M16 lane roles: pixel / channel l16 of a 16-tile, k-group g16 -> (term plane, 8-channel half)
+  const int l16 = lane & 15, g16 = lane >> 4, hh16 = g16 & 1;
+  int acol16[2][3];
+#pragma unroll
+  for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) acol16[pt][kx] = ((x0 + 16 * pt + l16 + kx - 1) >> (UP - 1)) - sx0 + 1;
+  const int apl1 = (g16 < 2 ? 0 : 1) * A_PLANE, apl2 = (g16 < 2 ? 0 : 2) * A_PLANE;  // [hi|mid], [hi|lo]
+  const int bpl1 = 0, bpl2 = g16 < 2 ? 1 : 0, bpl3 = g16 < 2 ? 2 : 1;  // [hi;hi], [mid;hi], [lo;mid]
 
   X3_LOAD(0);
   X3_STORE(0);
@@ -727,38 +767,75 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   for (int kc = 0; kc < nch; ++kc) {
     if (kc + 1 < nch) X3_LOAD(kc + 1);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (M16) {
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      bf16x8 bfr[3][RN][3];
+      for (int kx = 0; kx < 3; ++kx) {
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
+        for (int ky = 0; ky < 3; ++ky) {
+          const int tap = ky * 3 + kx;
+          bf16x8 g1[Q], g2[Q], g3[Q];
 #pragma unroll
-        for (int j = 0; j < RN; ++j)
+          for (int q = 0; q < Q; ++q) {
+            const int col = q * 16 + l16;
+            g1[q] = __builtin_bit_cast(bf16x8, Bs[((bpl1 * 9 + tap) * 2 + hh16) * BN + col]);
+            g2[q] = __builtin_bit_cast(bf16x8, Bs[((bpl2 * 9 + tap) * 2 + hh16) * BN + col]);
+            g3[q] = __builtin_bit_cast(bf16x8, Bs[((bpl3 * 9 + tap) * 2 + hh16) * BN + col]);
+          }
+#pragma unroll
+          for (int i = 0; i < RM; ++i) {
+            const int srow = (hh16 * SR + srow0 + x3_srel<UP>(i, ky)) * SC;
+            bf16x8 f1[2], f2[2];
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) {
+              f1[pt] = __builtin_bit_cast(bf16x8, As[apl1 + srow + acol16[pt][kx]]);
+              f2[pt] = __builtin_bit_cast(bf16x8, As[apl2 + srow + acol16[pt][kx]]);
+            }
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+              for (int q = 0; q < Q; ++q) {
+                f32x4v c = acc16[i][pt][q];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g3[q], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[pt], g2[q], c, 0, 0, 0);
+                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g1[q], c, 0, 0, 0);
+              }
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        bf16x8 bfr[3][RN][3];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+              bfr[ky][j][p] = __builtin_bit_cast(bf16x8, Bs[((p * 9 + ky * 3 + kx) * 2 + h) * BN + j * 32 + l32]);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          bf16x8 af[3];
 #pragma unroll
           for (int p = 0; p < 3; ++p)
-            bfr[ky][j][p] = __builtin_bit_cast(bf16x8, Bs[((p * 9 + ky * 3 + kx) * 2 + h) * BN + j * 32 + l32]);
+            af[p] = __builtin_bit_cast(bf16x8, As[p * A_PLANE + (h * SR + srow0 + s) * SC + acol[kx]]);
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        bf16x8 af[3];
+          for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
-          af[p] = __builtin_bit_cast(bf16x8, As[p * A_PLANE + (h * SR + srow0 + s) * SC + acol[kx]]);
+            for (int ky = 0; ky < 3; ++ky) {
+              if (x3_srel<UP>(i, ky) != s) continue;
 #pragma unroll
-        for (int i = 0; i < RM; ++i)
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky) {
-            if (x3_srel<UP>(i, ky) != s) continue;
-#pragma unroll
-            for (int j = 0; j < RN; ++j) {
-              f32x16 c = acc[i][j];
-              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[ky][j][0], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[ky][j][2], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[ky][j][1], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[ky][j][0], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[ky][j][1], c, 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[ky][j][0], c, 0, 0, 0);
+              for (int j = 0; j < RN; ++j) {
+                f32x16 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bfr[ky][j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[ky][j][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[ky][j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bfr[ky][j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[ky][j][1], c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bfr[ky][j][0], c, 0, 0, 0);
+              }
             }
-          }
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -770,13 +847,43 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   }
 #undef X3_LOAD
 #undef X3_STORE
+  if constexpr (M16) {
+    // staged epilogue, 32 channels (two 16-tiles) per pass: lane (l16, g16) holds pixels 16 pt + 4 g16
+    // + r of channel 16 q + l16 -> one float4 per (row, pixel tile) into the region
+    __syncthreads();  // every wave is done reading the last chunk's tiles
+    float* region = reinterpret_cast<float*>(x3_smem) + wm * 32 * RM * 36;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        const int q = 2 * j + qq, co = n0 + 16 * q + l16;
+        const float bv = (co < a.Cout && a.bias) ? a.bias[co] : 0.f;
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int pt = 0; pt < 2; ++pt) {
+            const f32x4v v = acc16[i][pt][q];
+            *reinterpret_cast<float4*>(region + ((16 * qq + l16) * RM + i) * 36 + 16 * pt + 4 * g16) =
+                make_float4(v[0] + bv, v[1] + bv, v[2] + bv, v[3] + bv);
+          }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_wave_barrier();
+      store_region<RM>(a, region, n, x0, y0, wm * RM, n0 + 32 * j, lane);
+      if (j + 1 < RN) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  } else {
 #if X3_STAGED_EPI
-  __syncthreads();  // every wave is done reading the last chunk's tiles
-  store_tiles_staged<RM, RN>(a, acc, n, x0, y0, wm * RM, n0, h, l32, lane,
-                             reinterpret_cast<float*>(x3_smem) + wm * 32 * RM * 36);
+    __syncthreads();  // every wave is done reading the last chunk's tiles
+    store_tiles_staged<RM, RN>(a, acc, n, x0, y0, wm * RM, n0, h, l32, lane,
+                               reinterpret_cast<float*>(x3_smem) + wm * 32 * RM * 36);
 #else
-  store_tiles<RM, RN>(a, acc, n, x0, y0, wm * RM, n0, h, l32);
+    store_tiles<RM, RN>(a, acc, n, x0, y0, wm * RM, n0, h, l32);
 #endif
+  }
 }
 
 // Direct (VALU) 3x3 conv for cout <= 4 — the decoder's final 64->3 conv (models.py:627). As a
@@ -1157,7 +1264,7 @@ int launch_cin4(const ConvArgs& a0, hipStream_t s, int up) {
   return (int)hipGetLastError();
 }
 
-template <int WM, int RM, int RN, int UP, int OCC>
+template <int WM, int RM, int RN, int UP, int OCC, bool M16>
 int launch_x3_one(const ConvArgs& a0, hipStream_t s) {
   using C = X3Cfg<WM, RM, RN, UP>;
   ConvArgs a = a0;
@@ -1167,7 +1274,7 @@ int launch_x3_one(const ConvArgs& a0, hipStream_t s) {
   const int64_t ntiles = (int64_t)a.tiles_x * a.tiles_y * a.N;
   const int64_t nblk = (ntiles + 7) / 8 * 8 * cdiv(a.Cout, C::BN);
   if (nblk >= 0x7fffffff) return AST_E_SHAPE;
-  auto kern = conv3x3_x3_kernel<WM, RM, RN, UP, OCC>;
+  auto kern = conv3x3_x3_kernel<WM, RM, RN, UP, OCC, M16>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
@@ -1178,11 +1285,11 @@ int launch_x3_one(const ConvArgs& a0, hipStream_t s) {
 }
 
 // split-bf16 MFMA kernel: no fused input normalisation (conv_1 runs the direct cin<=4 kernel)
-template <int WM, int RM, int RN, int OCC = 1>
+template <int WM, int RM, int RN, int OCC = 1, bool M16 = false>
 int launch_x3(const ConvArgs& a, hipStream_t s, int up) {
   if (a.in_mean) return AST_E_UNSUPPORTED;
   if ((int64_t)a.Cin * a.Hin * a.Win * 4 >= ((int64_t)1 << 31)) return AST_E_UNSUPPORTED;  // 32-bit buffer offsets
-  return up == 2 ? launch_x3_one<WM, RM, RN, 2, OCC>(a, s) : launch_x3_one<WM, RM, RN, 1, OCC>(a, s);
+  return up == 2 ? launch_x3_one<WM, RM, RN, 2, OCC, M16>(a, s) : launch_x3_one<WM, RM, RN, 1, OCC, M16>(a, s);
 }
 
 struct CfgEntry {
@@ -1225,6 +1332,11 @@ const CfgEntry kConfigs[] = {
     {launch_x3<4, 2, 2>, 64, 8, 2, 0},                  // 25: 8x32 px x 64 ch, 4 waves
     {launch_x3<4, 2, 1, 2>, 32, 8, 2, 0},               // 26: 8x32 px x 32 ch, 4 waves, 2 workgroups/CU
     {launch_x3<8, 2, 1, 1>, 32, 16, 2, 0},              // 27: 16x32 px x 32 ch, 8 waves
+    // the same tiles on the 16x16x32 bf16 MFMA (three K-32 products per block)
+    {launch_x3<8, 2, 2, 1, true>, 64, 16, 2, 0},        // 28: as 24
+    {launch_x3<4, 2, 2, 1, true>, 64, 8, 2, 0},         // 29: as 25
+    {launch_x3<4, 2, 1, 2, true>, 32, 8, 2, 0},         // 30: as 26
+    {launch_x3<8, 2, 1, 1, true>, 32, 16, 2, 0},        // 31: as 27
 };
 constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -1302,6 +1414,12 @@ int ast_conv3x3_fwd_f32_cfg(int cfg, const float* x, const float* x2, int n2, co
   if ((int64_t)round_up(cin, kCinAlign) * 9 * round_up(cout, kCoutAlign) >= ((int64_t)1 << 31)) return AST_E_SHAPE;
   if (cfg < 0) cfg = auto_config(cin, cout, n + n2, H, W, upsample, y_pool != nullptr, in_mean != nullptr);
   if (cfg >= kNumConfigs) return AST_E_UNSUPPORTED;
+  static const int m16 = [] {  // AST_CONV_M16=0|1: the split-bf16 tiles (24-27) on the 32x32x16 | 16x16x32 MFMA
+    const char* v = getenv("AST_CONV_M16");
+    return v ? atoi(v) : 1;
+  }();
+  if (cfg >= 24 && cfg <= 27 && m16 == 1) cfg += 4;
+  if (cfg >= 28 && cfg <= 31 && m16 == 0) cfg -= 4;
   const CfgEntry& e = kConfigs[cfg];
   if (y_pool && (e.rm % 2 != 0 || e.max_cout)) return AST_E_UNSUPPORTED;
   if (e.max_cout && cout > e.max_cout) return AST_E_UNSUPPORTED;

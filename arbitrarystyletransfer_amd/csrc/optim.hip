@@ -75,8 +75,16 @@ __global__ void norm_finish_kernel(const float* __restrict__ partial, long long 
 
 // torch foreach Adam: exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
 // denom = sqrt(exp_avg_sq) / sqrt(bc2) + eps; p.addcdiv_(exp_avg, denom, -lr/bc1).
+// sched != null (graph-capturable form): the step count and the bias-correction scalars come from
+// device memory (sched[1] != 0: skip the step), written by adam_sched_kernel just before.
 __global__ void adam_kernel(const TensorEntry* __restrict__ t, int nt, const float* __restrict__ state, float lr,
-                            float w1, float beta2, float w2, float eps, float step_size, float bc2_sqrt) {
+                            float w1, float beta2, float w2, float eps, float step_size, float bc2_sqrt,
+                            const float* __restrict__ sched) {
+  if (sched) {
+    if (sched[1] != 0.f) return;  // non-finite gradient norm: nothing changes (torch raises first)
+    step_size = sched[2];
+    bc2_sqrt = sched[3];
+  }
   const long long chunk = blockIdx.x;
   const TensorEntry e = t[find_entry(t, nt, chunk)];
   const long long b = (chunk - e.chunk0) * kChunk;
@@ -96,6 +104,28 @@ __global__ void adam_kernel(const TensorEntry* __restrict__ t, int nt, const flo
     const float denom = sqrtf(v) / bc2_sqrt + eps;
     e.p[i] = e.p[i] + (-step_size) * (m / denom);
   }
+}
+
+// sched = [step, skip, lr / bc1, sqrt(bc2)]: one thread advances the device step count and computes
+// the bias corrections in double, as torch's Python scalars (skip, step unchanged, when check_finite
+// and the gradient norm state[0] is not finite)
+__global__ void adam_sched_kernel(const float* __restrict__ state, double lr, double beta1, double beta2,
+                                  int check_finite, float* __restrict__ sched) {
+  if (threadIdx.x != 0) return;
+  if (check_finite && state) {
+    const float nrm = state[0];
+    if (!(fabsf(nrm) <= 3.402823466e38f)) {
+      sched[1] = 1.f;
+      return;
+    }
+  }
+  const float step = sched[0] + 1.f;
+  sched[0] = step;
+  sched[1] = 0.f;
+  const double bc1 = 1.0 - pow(beta1, (double)step);
+  const double bc2 = 1.0 - pow(beta2, (double)step);
+  sched[2] = (float)(lr / bc1);
+  sched[3] = (float)sqrt(bc2);
 }
 
 __global__ void grad_scale_kernel(const TensorEntry* __restrict__ t, int nt, const float* __restrict__ state) {
@@ -160,7 +190,19 @@ int ast_adam_step_f32(const void* dev_table, int ntensors, long long nchunks, co
   const double bc2 = 1.0 - pow(beta2, step);
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, (hipStream_t)stream,
                      (const TensorEntry*)dev_table, ntensors, state, (float)lr, (float)(1.0 - beta1), (float)beta2,
-                     (float)(1.0 - beta2), (float)eps, (float)(lr / bc1), (float)sqrt(bc2));
+                     (float)(1.0 - beta2), (float)eps, (float)(lr / bc1), (float)sqrt(bc2), nullptr);
+  return (int)hipGetLastError();
+}
+
+int ast_adam_step_sched_f32(const void* dev_table, int ntensors, long long nchunks, const float* state, double lr,
+                            double beta1, double beta2, double eps, float* sched, int check_finite, void* stream) {
+  if (!dev_table || !sched) return AST_E_NULLPTR;
+  if (ntensors <= 0 || nchunks <= 0 || nchunks > 0x7fffffffLL) return AST_E_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(adam_sched_kernel, dim3(1), dim3(64), 0, s, state, lr, beta1, beta2, check_finite ? 1 : 0, sched);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, (const TensorEntry*)dev_table,
+                     ntensors, state, (float)lr, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
+                     0.f, 1.f, (const float*)sched);
   return (int)hipGetLastError();
 }
 

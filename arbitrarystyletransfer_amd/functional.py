@@ -33,7 +33,7 @@ class TFPackCache:
 
     def get(self, weight: torch.Tensor, in_scale=None) -> torch.Tensor:
         w = _dev(weight.detach(), "weight")
-        key = (weight.data_ptr(), weight._version, ops.WEIGHTS_EPOCH[0],
+        key = (weight.data_ptr(), weight._version, ops.weight_epoch(weight),
                None if in_scale is None else (in_scale.data_ptr(), in_scale._version))
         hit = getattr(weight, "_ast_tf_pack", None)
         if hit is not None and hit[0] == key:

@@ -94,7 +94,7 @@ def _act_input(x: torch.Tensor, dt: torch.dtype, name: str = "x") -> torch.Tenso
 
 def _stamp(module: nn.Module, dt, device):
     ts = list(module.parameters()) + list(module.buffers())
-    return (dt, device, ops.WEIGHTS_EPOCH[0]) + tuple((t.data_ptr(), t._version) for t in ts)
+    return (dt, device) + tuple((t.data_ptr(), t._version, ops.weight_epoch(t)) for t in ts)
 
 
 class _Conv3x3HS(nn.Sequential):

@@ -127,7 +127,7 @@ class _PackedConvCache:
     def get(self, conv: nn.Conv2d) -> torch.Tensor:
         w = conv.weight
         key = id(conv)
-        stamp = (w.data_ptr(), w._version, w.device, ops.WEIGHTS_EPOCH[0])
+        stamp = (w.data_ptr(), w._version, w.device, ops.weight_epoch(w))
         hit = self._cache.get(key)
         if hit is not None and hit[0] == stamp:
             return hit[1]
@@ -228,6 +228,15 @@ class PretrainedEncoder(nn.Module):
             outs.extend(by_name[nm] for nm in collect)
             cur, cur2 = (pool if want_pool else act), None
         return outs
+
+    def prepack(self):
+        """Build the forward and input-gradient weight packs of every conv this network runs, ahead
+        of a hipGraph capture (train.StepGraph): the loss network is frozen, so its packs are made
+        once, outside the graph, instead of being rebuilt by every replay."""
+        norm = self._vgg_layers[0]
+        for idx, conv, *_ in self._plan():
+            self._packed.get(conv)
+            Fn._TF.get(conv.weight, norm.std.view(-1) if idx == 1 else None)
 
     def _forward_autograd(self, x):
         """Same walk through EncoderConvFn (HIP forward + HIP backward; the pre-ReLU output is
@@ -443,8 +452,8 @@ class Decoder(nn.Module):
                              f"got {tuple(x.shape)} {x.dtype} on {x.device}")
         x = x.contiguous()
         n, _, h, w = x.shape
-        stamp = (dt, x.device, ops.WEIGHTS_EPOCH[0], conv.weight._version, conv.bias._version,
-                 conv.weight.data_ptr())
+        stamp = (dt, x.device, ops.weight_epoch(conv.weight), ops.weight_epoch(conv.bias), conv.weight._version,
+                 conv.bias._version, conv.weight.data_ptr())
         if getattr(self, "_out_stamp", None) != stamp:
             self._w = conv.weight.detach().float().contiguous()
             self._b = conv.bias.detach().float().contiguous()

@@ -16,12 +16,20 @@ from ._lib import HipOpError, check, lib, ptr, stream_ptr
 PAD_MODES = {"zeros": 0, "reflect": 1}
 
 # Bumped by optimizers that update parameters through raw pointers (optim.FusedAdam), which
-# torch's per-tensor _version counter cannot see; weight-pack caches key on it.
+# torch's per-tensor _version counter cannot see; weight-pack caches key on it. Per parameter
+# (`_ast_epoch`), so the packs of frozen weights (the VGG loss network) survive optimizer steps.
 WEIGHTS_EPOCH = [0]
 
 
-def bump_weights_epoch():
+def bump_weights_epoch(params=None):
     WEIGHTS_EPOCH[0] += 1
+    for p in params or ():
+        p._ast_epoch = getattr(p, "_ast_epoch", 0) + 1
+
+
+def weight_epoch(t) -> int:
+    """The update count of parameter t by raw-pointer optimizers (cache keys)."""
+    return getattr(t, "_ast_epoch", 0)
 
 
 class LaunchTimer:

@@ -129,8 +129,85 @@ class FusedAdam(torch.optim.Optimizer):
             check(lib().ast_adam_step_f32(ptr(table.dev), len(params), nchunks, ptr(state), float(group["lr"]),
                                           float(b1), float(b2), float(group["eps"]), step, stream_ptr(dev)),
                   "adam_step")
-        ops.bump_weights_epoch()
+        ops.bump_weights_epoch([p for _, _, ps in groups for p in ps])
         return loss
+
+    # ---- graph-capturable step (hipGraph replays: no host sync, no allocation, device step count) --
+    def prepare_static(self):
+        """Before capture: moments, device tables (contents filled by fill_static once the
+        gradients' storage is known), the norm / schedule scratch and the device step count."""
+        self._static = []
+        dev = None
+        for group in self.param_groups:
+            params = list(group["params"])
+            dev = params[0].device
+            for p in params:
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            table = _Table()
+            nbytes = int(lib().ast_optim_table_bytes(len(params)))
+            table.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+            table.dev = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            nchunks = sum(-(-p.numel() // 65536) for p in params)
+            sched = torch.zeros(4, device=dev, dtype=torch.float32)
+            sched[0] = float(self.state[params[0]]["step"])
+            self._static.append((group, params, table, nchunks, sched))
+        allp = [p for _, ps, _, _, _ in self._static for p in ps]
+        if len(self._static) == 1:
+            self._static_norm = (self._static[0][2], len(allp), self._static[0][3])
+        else:
+            t = _Table()
+            nbytes = int(lib().ast_optim_table_bytes(len(allp)))
+            t.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+            t.dev = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            self._static_norm = (t, len(allp), sum(-(-p.numel() // 65536) for p in allp))
+        self._static_partial = torch.empty(self._static_norm[2], device=dev, dtype=torch.float32)
+        self._static_state = torch.zeros(2, device=dev, dtype=torch.float32)
+
+    def fill_static(self):
+        """After capture: write the tables (every parameter now holds its persistent gradient)."""
+        dev = None
+        for group, params, table, nchunks, _ in self._static:
+            if any(p.grad is None for p in params):
+                raise RuntimeError("FusedAdam.fill_static: a parameter has no gradient after the captured backward")
+            dev = params[0].device
+            n = table.build([p.data for p in params], [ops._dev(p.grad, "grad") for p in params],
+                            [self.state[p]["exp_avg"] for p in params], [self.state[p]["exp_avg_sq"] for p in params],
+                            dev)
+            assert n == nchunks
+        if len(self._static) > 1:
+            t, n_all, nchunks = self._static_norm
+            allp = [p for _, ps, _, _, _ in self._static for p in ps]
+            assert t.build([p.data for p in allp], [p.grad for p in allp], None, None, dev) == nchunks
+        torch.cuda.current_stream(dev).synchronize()   # the pinned tables have reached the device
+
+    def step_static(self):
+        """clip_grad_norm_ + Adam on the static tables, capturable: a non-finite norm skips the
+        update on the device (the caller checks last_grad_norm after the replay and raises)."""
+        dev = self._static[0][1][0].device
+        state = None
+        if self.max_grad_norm is not None:
+            table, n_all, nchunks = self._static_norm
+            check(lib().ast_grad_norm_f32(ptr(table.dev), n_all, nchunks, ptr(self._static_partial),
+                                          float(self.max_grad_norm), ptr(self._static_state), stream_ptr(dev)),
+                  "grad_norm")
+            state = self._static_state
+            self.last_grad_norm = state[0]
+        for group, params, table, nchunks, sched in self._static:
+            b1, b2 = group["betas"]
+            check(lib().ast_adam_step_sched_f32(ptr(table.dev), len(params), nchunks, ptr(state), float(group["lr"]),
+                                                float(b1), float(b2), float(group["eps"]), ptr(sched),
+                                                1 if self.error_if_nonfinite else 0, stream_ptr(dev)), "adam_step")
+
+    def after_static_step(self):
+        """Host bookkeeping of one replayed step (after the caller's non-finite check)."""
+        for _, params, _, _, _ in self._static:
+            for p in params:
+                self.state[p]["step"] += 1
+        ops.bump_weights_epoch([p for _, ps, _, _, _ in self._static for p in ps])
 
 
 def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=False):

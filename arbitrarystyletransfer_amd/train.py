@@ -39,9 +39,62 @@ import torch.distributed as dist
 
 from . import dp
 from . import losses as L
-from . import models
+from . import models, ops
 from .conf import enc_out_layers
 from .optim import FusedAdam
+
+class StepGraph:
+    """One training step captured in a hipGraph (torch.cuda.CUDAGraph is the HIP graph on ROCm):
+    forward, backward, the gradient-arena reduction and clip + Adam replay with no Python, no
+    launch latency and no host sync (every C-ABI call is capture-safe: no allocation, no sync).
+    Inputs are copied into static buffers before each replay; the outputs are the captured
+    step's static tensors. Gradients live in a flat arena (dp.FlatGradArena) so the optimizer's
+    device tables point at storage that stays put; its step count and bias corrections are
+    computed on the device (optim.FusedAdam.step_static). The one host sync left is the
+    non-finite gradient-norm check (train.py:292, clip_grad_norm_(error_if_nonfinite))."""
+
+    def __init__(self, optim, arena, params, body, frozen=()):
+        self.optim, self.arena, self.params, self.body = optim, arena, list(params), body
+        self.frozen = list(frozen)   # frozen networks whose weight packs are built once, outside the graph
+        self.graph = None
+        self.shapes = None
+
+    def _capture(self, inputs):
+        for net in self.frozen:
+            net.prepack()
+        self.optim.zero_grad(set_to_none=True)
+        self.arena.reset()
+        # every trainable weight's pack is rebuilt inside the graph (replays update the weights)
+        ops.bump_weights_epoch(self.params)
+        self.optim.prepare_static()
+        self.static = [torch.empty_like(x) for x in inputs]
+        for s_, x in zip(self.static, inputs):
+            s_.copy_(x)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.out = self.body(*self.static)
+        self.optim.fill_static()
+        self.graph = g
+        self.shapes = [tuple(x.shape) for x in inputs]
+
+    def run(self, *inputs):
+        if self.graph is None or self.shapes != [tuple(x.shape) for x in inputs]:
+            self._capture(inputs)
+        for s_, x in zip(self.static, inputs):
+            s_.copy_(x)
+        self.graph.replay()
+        if self.optim.error_if_nonfinite:
+            v = float(self.optim.last_grad_norm.item())   # the one host sync per step
+            if v != v or v in (float("inf"), float("-inf")):
+                raise RuntimeError(f"The total norm of order 2.0 for gradients from `parameters` is non-finite ({v}), "
+                                   "so it cannot be clipped (error_if_nonfinite=True, train.py:292); the step was "
+                                   "not applied")
+        self.optim.after_static_step()
+        out = dict(self.out)
+        out["grad_norm"] = self.optim.last_grad_norm
+        return out
+
 
 STYLE_WEIGHTS = (1.0, 1.0, 1.0, 1.0, 0.75, 0.5)   # train.py:232-238 for the 6 loss-network layers
 LOSSNET_LAYERS = ["conv_1", "conv_3", "conv_5", "conv_9", "conv_13", "relu_15"]   # models.py:187
@@ -215,7 +268,8 @@ class ASTTrainer:
     Data parallel as AdaINTrainer (args.batch_size = global batch, shard-weighted batch-mean terms,
     one SUM all-reduce of the flat gradient arena) plus SyncBatchNorm for the train-mode encoder."""
 
-    def __init__(self, args=None, device=None, ast=None, lossnet=None, content_iter=None, grad_hook=None):
+    def __init__(self, args=None, device=None, ast=None, lossnet=None, content_iter=None, grad_hook=None,
+                 graph=None):
         self.args = args or default_ast_args()
         self.device = torch.device(device or "cuda")
         self.ast = (ast or models.AST(attention=True)).to(self.device).train()
@@ -235,6 +289,15 @@ class ASTTrainer:
             dp.shard_range(self.args.batch_size, self.rank, self.world)
             dp.convert_sync_batchnorm(self.ast)
             self.grad_arena = dp.FlatGradArena(self.params, average=False)
+        # graph mode (default on: the step is launch-bound at the reference's 160^2 training size):
+        # the whole step replays as one hipGraph (StepGraph); grad_hook is then not called
+        self.graph = (getattr(self.args, "graph", True) if graph is None else graph) and grad_hook is None
+        self._step_graph = None
+        if self.graph:
+            if self.grad_arena is None:   # persistent gradient storage for the captured optimizer tables
+                self.grad_arena = dp.FlatGradArena(self.params, average=False)
+            self._step_graph = StepGraph(self.ast_optim, self.grad_arena, self.params, self._step_body,
+                                         frozen=[self.pretrained_enc])
         self.train_dict = {"content_loss": [], "style_loss": [], "lf_loss": [], "tv_loss": [], "org_img_loss": []}
         self.save_file = os.path.join(self.args.save_dir, "ast.pth")
         self.train_dict_file = os.path.join(self.args.save_dir, "ast_train_dict.json")
@@ -284,22 +347,35 @@ class ASTTrainer:
                 "lf_loss": lf_loss, "tv_loss": tv, "org_img_loss": org_img_loss, "hist_loss": hist_loss,
                 "out_of_range_loss": range_loss, "stylized": stylized, "t": t, "org_out": org_out}
 
-    def train_step(self, content, style, record=False):
-        out = self.compute_losses(content, style)
-        self.ast_optim.zero_grad(set_to_none=True)                                      # :287
+    def _backward(self, out, n_local):
         if self.world == 1:
             out["loss"].backward()                                                      # :288
         else:
             a, b = dp.shard_range(self.args.batch_size, self.rank, self.world)
-            if content.shape[0] != b - a:
-                raise ValueError(f"rank {self.rank} holds {content.shape[0]} images, its shard is {b - a}")
+            if n_local != b - a:
+                raise ValueError(f"rank {self.rank} holds {n_local} images, its shard is {b - a}")
             ((b - a) / self.args.batch_size * out["_mean_terms"] + self.args.tv_lam * out["tv_loss"]).backward()
         if self.grad_arena is not None:
             self.grad_arena.all_reduce()
-        if self.grad_hook is not None:
-            self.grad_hook(self.params)
-        self.ast_optim.step()                                                           # :292, :300
-        out["grad_norm"] = self.ast_optim.last_grad_norm
+
+    def _step_body(self, content, style):
+        """The captured step (StepGraph): losses, backward, reduction, clip + Adam."""
+        out = self.compute_losses(content, style)
+        self._backward(out, content.shape[0])
+        self.ast_optim.step_static()
+        return out
+
+    def train_step(self, content, style, record=False):
+        if self.graph:
+            out = self._step_graph.run(content, style)
+        else:
+            out = self.compute_losses(content, style)
+            self.ast_optim.zero_grad(set_to_none=True)                                  # :287
+            self._backward(out, content.shape[0])
+            if self.grad_hook is not None:
+                self.grad_hook(self.params)
+            self.ast_optim.step()                                                       # :292, :300
+            out["grad_norm"] = self.ast_optim.last_grad_norm
         if record:                                                                      # :302-306
             keys = ("content_loss", "style_loss", "lf_loss", "tv_loss", "org_img_loss")
             w = 1.0 if self.world == 1 else dp.shard_weight(self.args.batch_size, self.rank, self.world)

@@ -177,7 +177,8 @@ def ae_train_bench(args, dev, rank, world):
         "roofline": {"bound": "mfma", "kernel": "loss-network conv3x3 fwd/dgrad launches of a step (split-bf16)",
                      "achieved": tf, "peak": PEAK_SPLIT_BF16_TF, "unit": "TFLOP/s", "frac": tf / PEAK_SPLIT_BF16_TF,
                      "fp32_mfma_peak": PEAK_FP32_MFMA_TF, "frac_of_fp32_mfma_peak": tf / PEAK_FP32_MFMA_TF,
-                     "traffic": None, "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3)},
+                     "traffic": None, "mfma_share_of_step": ms / args.steps / (elapsed / steps_timed * 1e3),
+                     "timing_source": "HIP events around each launch of 3 eager steps of the same shapes"},
         "kernels_ms_per_step": {k: round(m / args.steps, 4) for k, (f, m, c) in sorted(fam.items())},
         "mbgemm_tflops": (fam["mbgemm"][0] / (fam["mbgemm"][1] * 1e-3) / 1e12) if "mbgemm" in fam else None,
     }
@@ -194,21 +195,20 @@ def ast_train_bench(args, dev, rank, world):
     all-reduce."""
     from arbitrarystyletransfer_amd.train import ASTTrainer, default_ast_args
     B, S = args.batch or 8, args.size or 160
+    graph = os.environ.get("AST_TRAIN_GRAPH", "1") != "0"
     trainer = ASTTrainer(default_ast_args(batch_size=B * world), device=dev,
-                         ast=models.AST(attention=True).load_live_init())
+                         ast=models.AST(attention=True).load_live_init(), graph=graph)
     content = torch.from_numpy(synth.image(905 + rank, (B, 3, S, S))).to(dev)
     style = torch.from_numpy(synth.image(925 + rank, (B, 3, S, S))).to(dev)
-    for _ in range(args.warmup):
+    for _ in range(args.warmup):   # the first step captures the hipGraph (graph mode)
         trainer.train_step(content, style, record=False)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    timer = ops.LaunchTimer()
     t0 = time.perf_counter()
-    with timer:
-        for _ in range(args.steps):
-            out = trainer.train_step(content, style, record=False)
+    for _ in range(args.steps):
+        out = trainer.train_step(content, style, record=False)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -217,6 +217,21 @@ def ast_train_bench(args, dev, rank, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     assert torch.isfinite(out["loss"]), "non-finite loss"
+    # per-kernel-family times: HIP events around every launch of an eager step (a replayed graph
+    # launches nothing from Python), same kernels and shapes as the timed steps
+    eager = ASTTrainer(default_ast_args(batch_size=B * world), device=dev,
+                       ast=models.AST(attention=True).load_live_init(), graph=False)
+    ksteps = 3
+    eager.train_step(content, style, record=False)
+    torch.cuda.synchronize(dev)
+    timer = ops.LaunchTimer()
+    te = time.perf_counter()
+    with timer:
+        for _ in range(ksteps):
+            eager.train_step(content, style, record=False)
+    torch.cuda.synchronize(dev)
+    eager_ms = (time.perf_counter() - te) / ksteps * 1e3
+    del eager
     fam = {}
     for tag, fl, ms in timer.results():
         k = tag.split()[0]
@@ -225,12 +240,15 @@ def ast_train_bench(args, dev, rank, world):
     mm = [fam[k] for k in fam if k.startswith(("conv3x3", "wgrad"))]
     fl, ms = sum(f for f, _, _ in mm), sum(m for _, m, _ in mm)
     tf = fl / (ms * 1e-3) / 1e12 if ms else 0.0
+    args.steps, steps_timed = ksteps, args.steps   # the per-step kernel figures below are per eager step
     result = {
         "metric": "AST training images/sec (train.py ASTTrainer step, MobileNet AST + AdaAttN)",
-        "value": B * world * args.steps / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "value": B * world * steps_timed / elapsed, "unit": "images/s", "n_gpus": world, "steps": steps_timed,
+        "warmup": args.warmup, "ms_per_step": elapsed / steps_timed * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (live-init weights, U[0,1) images), resident in HBM",
+        "step_mode": "hipGraph replay (train.StepGraph)" if graph else "eager",
+        "eager_ms_per_step": eager_ms,
         "config": {"workload": f"ASTTrainer step (MobileNet AST + AdaAttN in train mode; content, style, lf, tv, hist, "
                                f"org_img, out_of_range losses via the VGG loss network; clip 2.0 + Adam), "
                                f"bs={B}/GPU {S}x{S} fp32",
@@ -239,7 +257,8 @@ def ast_train_bench(args, dev, rank, world):
         "roofline": {"bound": "mfma", "kernel": "loss-network conv3x3 fwd/dgrad launches of a step (split-bf16)",
                      "achieved": tf, "peak": PEAK_SPLIT_BF16_TF, "unit": "TFLOP/s", "frac": tf / PEAK_SPLIT_BF16_TF,
                      "fp32_mfma_peak": PEAK_FP32_MFMA_TF, "frac_of_fp32_mfma_peak": tf / PEAK_FP32_MFMA_TF,
-                     "traffic": None, "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3)},
+                     "traffic": None, "mfma_share_of_step": ms / args.steps / (elapsed / steps_timed * 1e3),
+                     "timing_source": "HIP events around each launch of 3 eager steps of the same shapes"},
         "kernels_ms_per_step": {k: round(m / args.steps, 4) for k, (f, m, c) in sorted(fam.items())},
         "mbgemm_tflops": (fam["mbgemm"][0] / (fam["mbgemm"][1] * 1e-3) / 1e12) if "mbgemm" in fam else None,
     }

@@ -265,6 +265,15 @@ int ast_grad_scale_f32(const void* dev_table, int ntensors, long long nchunks, c
 int ast_adam_step_f32(const void* dev_table, int ntensors, long long nchunks, const float* state,
                       double lr, double beta1, double beta2, double eps, int step, void* stream);
 
+/* The same step with its step count on the device (hipGraph replays): sched [4] floats =
+ * [step count, skip flag, lr / bias_correction1, sqrt(bias_correction2)]; the call advances
+ * sched[0] and computes the rest on the device. check_finite: a non-finite gradient norm state[0]
+ * sets the skip flag and leaves parameters, moments, gradients and the step count unchanged (the
+ * caller reads state[0] after the step and raises, as clip_grad_norm_(error_if_nonfinite)). */
+int ast_adam_step_sched_f32(const void* dev_table, int ntensors, long long nchunks, const float* state,
+                            double lr, double beta1, double beta2, double eps, float* sched, int check_finite,
+                            void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * MobileNet-style variant (config 5). dtype / dtype_in / dtype_out: 0 = fp32,
  * 1 = bf16 storage (fp32 accumulate). All maps NCHW contiguous. BatchNorm (eval) is folded into

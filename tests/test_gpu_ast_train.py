@@ -210,3 +210,36 @@ def test_ast_trainer_dp_uneven_matches_single_process(tmp_path, hip_device):
     for n, b in tr.ast.named_buffers():
         if b.is_floating_point():
             assert rel_inf(got[f"buf:{n}"], b) <= 1e-4, n
+
+
+def test_ast_trainer_graph_matches_eager(hip_device):
+    """ASTTrainer's hipGraph mode (train.StepGraph: the whole step -- forward, backward, gradient
+    arena, clip + Adam with the step count on the device -- replayed as one graph) against the
+    eager step: two steps from the same initial state give the same losses, gradient norms and
+    parameters (bitwise: the same kernels run in the same order; the Adam bias corrections are
+    computed on the device in double, as the host does, allowed one fp32 ulp). A non-finite
+    gradient norm raises after the replay and leaves every parameter unchanged."""
+    from arbitrarystyletransfer_amd.train import ASTTrainer, default_ast_args
+    c = torch.from_numpy(synth.image(971, (2, 3, 64, 64))).to(hip_device)
+    s = torch.from_numpy(synth.image(972, (2, 3, 64, 64))).to(hip_device)
+    runs = {}
+    for graph in (False, True):
+        torch.manual_seed(0)
+        tr = ASTTrainer(default_ast_args(batch_size=2), device=hip_device,
+                        ast=models.AST(attention=True).load_live_init(), graph=graph)
+        assert tr.graph == graph
+        outs = [tr.train_step(c, s, record=True) for _ in range(2)]
+        runs[graph] = (tr, [(float(o["loss"]), float(o["grad_norm"])) for o in outs],
+                       [p.detach().clone() for p in tr.params], dict(tr.train_dict))
+    (te, le, pe, de), (tg, lg, pg, dg) = runs[False], runs[True]
+    assert le == lg, (le, lg)
+    assert de == dg
+    for a, b in zip(pe, pg):
+        assert torch.allclose(a, b, rtol=2e-7, atol=0), float((a - b).abs().max())
+    before = [p.detach().clone() for p in tg.params]
+    bad = c.clone()
+    bad[0, 0, 5, 5] = float("nan")
+    with pytest.raises(RuntimeError, match="non-finite"):
+        tg.train_step(bad, s)
+    for a, b in zip(before, tg.params):
+        assert torch.equal(a, b.detach())
