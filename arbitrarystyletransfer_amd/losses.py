@@ -1,14 +1,30 @@
 """Drop-in for the reference losses.py: gram_matrix, compute_content_loss, compute_style_loss,
 tv_loss and the soft-histogram / Earth-Mover loss compute_hist_loss
 (losses.py:8-87; §8f "next" #2), with the SingleDimHistLayer / EarthMoversDistanceLoss modules
-and the module-level `hist` / `earth_movers` instances. Forward and backward are HIP kernels
-(functional.py)."""
+and the module-level `hist` / `earth_movers` instances. Every loss is a torch.ops.ast_hip custom op
+(library.py) whose forward and backward are HIP kernels: one fused launch for the value, one for
+the gradient."""
 from __future__ import annotations
 
 from . import functional as Fn
+from . import library  # noqa: F401  (registers torch.ops.ast_hip.*)
+from .ops import _dev
 
 import torch
 import torch.nn as nn
+
+_ops = torch.ops.ast_hip
+
+
+def _grad(x):
+    return torch.is_grad_enabled() and x.requires_grad
+
+
+def _pair(x, y, what):
+    x, y = _dev(x, "input"), _dev(y, "target")
+    if x.shape != y.shape:
+        raise Fn.HipOpError(f"{what}: shape mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
+    return x, y
 
 __all__ = ["gram_matrix", "compute_content_loss", "compute_style_loss", "tv_loss", "compute_hist_loss",
            "content_mvn_loss", "style_loss_weighted", "EarthMoversDistanceLoss", "HistLayerBase",
@@ -17,34 +33,38 @@ __all__ = ["gram_matrix", "compute_content_loss", "compute_style_loss", "tv_loss
 
 def gram_matrix(tensor):
     """losses.py:105-109: bmm(F, F^T) / (C*H*W), F = tensor.view(B, C, H*W)."""
-    return Fn.GramFn.apply(tensor)
+    return _ops.gram(_dev(tensor, "tensor"))
 
 
 def compute_content_loss(inp, tgt):
     """losses.py:124-126: F.huber_loss(inp, tgt) (delta 1, mean)."""
-    return Fn.HuberFn.apply(inp, tgt)
+    return _ops.huber_loss(*_pair(inp, tgt, "huber"))
 
 
 def compute_style_loss(t_cs_map, style_map):
     """losses.py:128-139: 1.25*huber(mean) + 1.25*huber(std) + 10*huber(gram). The target is
     treated as a constant (train.py:233 always passes style_map[i].detach())."""
-    return Fn.StyleLossFn.apply(t_cs_map, style_map.detach(), 1.0)
+    return style_loss_weighted(t_cs_map, style_map, 1.0)
 
 
 def tv_loss(img):
     """losses.py:90-103: sum of squared horizontal and vertical neighbour differences."""
-    return Fn.TVLossFn.apply(img)
+    return _ops.tv_loss(_dev(img, "img"))
 
 
 def content_mvn_loss(inp, tgt, weight: float = 1.0):
     """weight * compute_content_loss(mean_variance_norm(inp), mean_variance_norm(tgt.detach()))
     in one fused kernel (train.py:223-227, 258, 277)."""
-    return Fn.MVNHuberFn.apply(inp, tgt.detach(), float(weight))
+    x, y = _pair(inp, tgt.detach(), "content loss")
+    return _ops.content_mvn_loss(x, y, float(weight), _grad(x))[0]
 
 
 def style_loss_weighted(t_cs_map, style_map, weight: float = 1.0):
     """weight * compute_style_loss(t_cs_map, style_map.detach()) (train.py:230-245, 271)."""
-    return Fn.StyleLossFn.apply(t_cs_map, style_map.detach(), float(weight))
+    x, y = _dev(t_cs_map, "x"), _dev(style_map.detach(), "y")
+    if x.shape[:2] != y.shape[:2] or x.shape[2:] != y.shape[2:]:
+        raise Fn.HipOpError(f"style loss: shape mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
+    return _ops.style_loss(x, y, float(weight), _grad(x))[0]
 
 
 class EarthMoversDistanceLoss(nn.Module):
@@ -79,14 +99,17 @@ earth_movers = EarthMoversDistanceLoss()   # losses.py:80
 def compute_hist_loss(t_cs, style_map, weight: float = 1.0):
     """losses.py:84-87: earth_movers(hist(t_cs), hist(style_map)).mean(), differentiable in t_cs
     (style_map is data, train.py:261). `weight` fuses the caller's scale (train.py: 1e-5)."""
-    return Fn.HistLossFn.apply(t_cs, style_map.detach(), float(weight))
+    x, y = _dev(t_cs, "t_cs"), _dev(style_map.detach(), "style_map")
+    if x.shape[0] != y.shape[0]:
+        raise Fn.HipOpError(f"hist loss: batch mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
+    return _ops.hist_loss(x, y, float(weight))[0]
 
 
 def out_of_range_loss(img, weight: float = 1e8):
     """train.py:259: compute_content_loss(img, torch.clip(img.detach(), 0.0, 1.0)) * 1e8."""
-    return Fn.RangeLossFn.apply(img, float(weight))
+    return _ops.range_loss(_dev(img, "x"), float(weight))
 
 
 def pixel_mse_loss(out, target, weight: float = 100.0):
     """train.py:268: ((target.detach() - out) ** 2).mean() * 100."""
-    return Fn.SqDiffMeanFn.apply(out, target.detach(), float(weight))
+    return _ops.sqdiff_mean(*_pair(out, target.detach(), "sqdiff"), float(weight))

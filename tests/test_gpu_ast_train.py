@@ -228,8 +228,11 @@ def test_ast_trainer_graph_matches_eager(hip_device):
         tr = ASTTrainer(default_ast_args(batch_size=2), device=hip_device,
                         ast=models.AST(attention=True).load_live_init(), graph=graph)
         assert tr.graph == graph
-        outs = [tr.train_step(c, s, record=True) for _ in range(2)]
-        runs[graph] = (tr, [(float(o["loss"]), float(o["grad_norm"])) for o in outs],
+        vals = []
+        for _ in range(2):   # graph mode: the outputs are the captured step's static tensors, read them now
+            o = tr.train_step(c, s, record=True)
+            vals.append((float(o["loss"]), float(o["grad_norm"])))
+        runs[graph] = (tr, vals,
                        [p.detach().clone() for p in tr.params], dict(tr.train_dict))
     (te, le, pe, de), (tg, lg, pg, dg) = runs[False], runs[True]
     assert le == lg, (le, lg)
