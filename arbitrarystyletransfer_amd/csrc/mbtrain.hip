@@ -5,7 +5,7 @@
 // composable kernels, each with its backward:
 //   gemm_kernel         strided-batched C (+)= A.B on MFMA-fp32 (1x1 convs: forward, input grad,
 //                       weight grad with the pixel/batch reduction split across workgroups)
-//   dw_fwd / dw_dgrad / dw_wgrad   depthwise kxk, stride 1|2, reflect padding
+//   (the depthwise kxk conv and its gradients are in mbt_dw.hip)
 //   bn_stats / bn_apply / bn_bwd_reduce / bn_bwd_apply   BatchNorm2d in training mode
 //   hardswish fwd/bwd, add, nearest upsample x2 fwd/bwd, plane means (SE pool)
 //   se_fc_fwd / se_fc_bwd  the SE MLP (Linear-ReLU-Linear-Hardtanh) per image in one workgroup
@@ -15,6 +15,7 @@
 #include <stdint.h>
 #include "../../include/ast_hip.h"
 #include "det.h"
+#include "x3.h"
 
 namespace {
 
@@ -207,168 +208,229 @@ __global__ __launch_bounds__(kT) void gemm_reduce_kernel(GemmArgs a, int zper) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// depthwise kxk conv with reflect padding p = (k-1)/2 (torch padding_mode="reflect"), stride s.
-// The host guarantees p < size, so one reflection suffices. Flat 32-bit thread index over
-// planes x pixels (host-checked < 2^31).
+// Split-bf16 GEMM (the default for the 1x1 convs): C = A.B with fp32 inputs carried as three bf16
+// terms (x3.h) and the six largest term products, folded into three v_mfma_f32_16x16x32_bf16 per 16
+// channels of K (conv3x3_igemm.hip's M16 scheme) -- fp32-level accuracy at 2.7x the fp32 MFMA rate,
+// so the skinny-K / skinny-MN shapes of a MobileNet block stay HBM-bound.
+// Tile BM (m) x BN (n), 4 waves of (BM/2) x (BN/2), K in chunks of 32. The MFMA's A operand is the
+// N side (B^T rows), its B operand the M side, so a lane's accumulator holds 4 consecutive n of one
+// m: the epilogue writes 16-byte vectors along n (C rows are n-contiguous in every caller).
+// LDS: per side [3 terms][rows][32 + 8] bf16 (80-byte rows: the b128 fragment reads of 16 rows hit
+// distinct banks). Staging: a thread owns (row, 8 consecutive k) items -- two 16-byte loads when k
+// is contiguous, else eight loads coalesced across the lanes' consecutive rows -- splits them and
+// writes one 16-byte vector per term; the next chunk's loads are in flight during the MFMAs.
+// Folded K (foldK = P) needs P % 8 == 0 so that 8 consecutive k stay in one image (host-checked).
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ int refl(int i, int n) {
-  i = i < 0 ? -i : i;
-  return i >= n ? 2 * (n - 1) - i : i;
-}
+constexpr int X3KC = 32, X3KP = X3KC + 8;
 
-// grid (pixel chunks of kT, planes strided by gridDim.y): the plane, hence the channel and its
-// K*K weights, is uniform per workgroup (scalar loads)
-template <int K, int S>
-__global__ __launch_bounds__(kT) void dw_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                    float* __restrict__ y, int planes, int c, int h, int wd, int ho,
-                                                    int wo) {
-  constexpr int P = (K - 1) / 2;
-  const int e = blockIdx.x * kT + threadIdx.x;
-  const int hwo = ho * wo;
-  const int oy = e / wo, ox = e - oy * wo;
-  int ix[K];
-#pragma unroll
-  for (int kx = 0; kx < K; ++kx) ix[kx] = refl(ox * S - P + kx, wd);
-  for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
-    const float* wc = w + (pl % c) * K * K;
-    float wr[K * K];
-#pragma unroll
-    for (int t = 0; t < K * K; ++t) wr[t] = wc[t];
-    if (e >= hwo) continue;
-    const float* xp = x + (int64_t)pl * h * wd;
-    float acc = 0.f;
-#pragma unroll
-    for (int ky = 0; ky < K; ++ky) {
-      const float* row = xp + refl(oy * S - P + ky, h) * wd;
-#pragma unroll
-      for (int kx = 0; kx < K; ++kx) acc = fmaf(wr[ky * K + kx], row[ix[kx]], acc);
+struct X3Flags {
+  int vecA, vecB, vecC, vecP;  // 16-byte paths legal: A / B k-runs, C / partial-tile n-runs
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(kT, 2) void gemm_x3_kernel(GemmArgs a, X3Flags f) {
+  using ast_x3::bf16;
+  using ast_x3::bf16x8;
+  using ast_x3::f32x4;
+  __shared__ __attribute__((aligned(16))) bf16 Ns[3][BN][X3KP];
+  __shared__ __attribute__((aligned(16))) bf16 Ms[3][BM][X3KP];
+  constexpr int WN = BN / 2, WM = BM / 2, TN = WN / 16, TM = WM / 16;
+  constexpr int NI = BN * 4 / kT, MI = BM * 4 / kT;  // staging items per thread
+  static_assert(NI >= 1 && MI >= 1 && BN * 4 % kT == 0 && BM * 4 % kT == 0, "tile");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave & 1, wm = wave >> 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int b = blockIdx.z / a.ksplit, ks = blockIdx.z % a.ksplit;
+  const int kbeg = ks * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
+  const float* A = a.A + b * a.sAb;
+  const float* B = a.B + b * a.sBb;
+  // k offsets: folded K walks images through the batch stride (batch == 1 then)
+  auto koffA = [&](int k) -> int64_t {
+    if (a.foldK) {
+      const int bb = k / a.foldK;
+      return bb * a.sAb + (int64_t)(k - bb * a.foldK) * a.sAk;
     }
-    y[(int64_t)pl * hwo + e] = acc;
-  }
-}
-
-// Input gradient = reflect_pad^T(conv^T(g)) in two passes, both branch-free in the bulk:
-//  dw_dpad_kernel: the gradient w.r.t. the PADDED input, dpad[q] = sum over taps t with
-//                  (q - t) = s * o for an output o of g[o] * w[t] (invalid taps masked by a zero
-//                  weight and a clamped address, so no lane diverges)
-//  dw_fold_kernel: dx[i] = dpad[i + p] + the pad positions that reflect onto i (per axis: top pad
-//                  p - i for 1 <= i <= p, bottom pad 2(n-1) - i + p for n-1-p <= i <= n-2).
-// Grids as dw_fwd_kernel (pixel chunks x planes).
-template <int K, int S>
-__global__ __launch_bounds__(kT) void dw_dpad_kernel(const float* __restrict__ g, const float* __restrict__ w,
-                                                     float* __restrict__ dpad, int planes, int c, int hp, int wp,
-                                                     int ho, int wo) {
-  const int e = blockIdx.x * kT + threadIdx.x;
-  const int qy = e / wp, qx = e - qy * wp;
-  int ox[K];     // clamped source column and 0/1 validity of each column tap (hoisted out of the planes)
-  float mx[K];
-#pragma unroll
-  for (int tx = 0; tx < K; ++tx) {
-    const int u = qx - tx;
-    mx[tx] = (u >= 0 && (u % S) == 0 && u / S < wo) ? 1.f : 0.f;
-    ox[tx] = min(max(u, 0) / S, wo - 1);
-  }
-  for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
-    const float* wc = w + (pl % c) * K * K;
-    float wr[K * K];
-#pragma unroll
-    for (int t = 0; t < K * K; ++t) wr[t] = wc[t];
-    if (e >= hp * wp) continue;
-    const float* gp = g + (int64_t)pl * ho * wo;
-    float acc = 0.f;
-#pragma unroll
-    for (int ty = 0; ty < K; ++ty) {
-      const int t = qy - ty;
-      const float my = (t >= 0 && (t % S) == 0 && t / S < ho) ? 1.f : 0.f;
-      const float* grow = gp + min(max(t, 0) / S, ho - 1) * wo;
-#pragma unroll
-      for (int tx = 0; tx < K; ++tx) acc = fmaf(grow[ox[tx]], wr[ty * K + tx] * (my * mx[tx]), acc);
+    return (int64_t)k * a.sAk;
+  };
+  auto koffB = [&](int k) -> int64_t {
+    if (a.foldK) {
+      const int bb = k / a.foldK;
+      return bb * a.sBb + (int64_t)(k - bb * a.foldK) * a.sBk;
     }
-    dpad[(int64_t)pl * hp * wp + e] = acc;
-  }
-}
-
-template <int P>
-__global__ __launch_bounds__(kT) void dw_fold_kernel(const float* __restrict__ dpad, float* __restrict__ dx, int planes,
-                                                     int h, int wd) {
-  const int hp = h + 2 * P, wp = wd + 2 * P;
-  const int e = blockIdx.x * kT + threadIdx.x;
-  if (e >= h * wd) return;
-  const int iy = e / wd, ix = e - iy * wd;
-  // per axis up to 3 padded preimages; -1 = none
-  const int y1 = (iy >= 1 && iy <= P) ? P - iy : -1;
-  const int y2 = (iy >= h - 1 - P && iy <= h - 2) ? 2 * (h - 1) - iy + P : -1;
-  const int x1 = (ix >= 1 && ix <= P) ? P - ix : -1;
-  const int x2 = (ix >= wd - 1 - P && ix <= wd - 2) ? 2 * (wd - 1) - ix + P : -1;
-  for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
-    const float* d = dpad + (int64_t)pl * hp * wp;
-    const int qy0 = iy + P, qx0 = ix + P;
-    float acc = d[qy0 * wp + qx0];
-    if (x1 >= 0) acc += d[qy0 * wp + x1];
-    if (x2 >= 0) acc += d[qy0 * wp + x2];
-    if (y1 >= 0) {
-      acc += d[y1 * wp + qx0];
-      if (x1 >= 0) acc += d[y1 * wp + x1];
-      if (x2 >= 0) acc += d[y1 * wp + x2];
-    }
-    if (y2 >= 0) {
-      acc += d[y2 * wp + qx0];
-      if (x1 >= 0) acc += d[y2 * wp + x1];
-      if (x2 >= 0) acc += d[y2 * wp + x2];
-    }
-    dx[(int64_t)pl * h * wd + e] = acc;
-  }
-}
-
-// part[c][n * segments + seg][tap] = sum over a segment of one image's output plane (grid =
-// (segments, n, c)); the K*K partial sums are reduced across the wave by shuffles, across the 4
-// waves through LDS; the host then sums each channel's (image, segment) rows in order.
-constexpr int DW_SEG = 8 * kT;
-
-template <int K, int S>
-__global__ __launch_bounds__(kT) void dw_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ g,
-                                                      float* __restrict__ part, int c, int h, int wd, int ho, int wo) {
-  constexpr int P = (K - 1) / 2, KK = K * K;
-  __shared__ float sh[4][KK];
-  const int ch = blockIdx.z, n = blockIdx.y;
-  const int64_t pl = (int64_t)n * c + ch;
-  const float* xp = x + pl * h * wd;
-  const float* gp = g + pl * ho * wo;
-  const int hwo = ho * wo;
-  const int beg = blockIdx.x * DW_SEG, end = min(hwo, beg + DW_SEG);
-  float acc[KK];
+    return (int64_t)k * a.sBk;
+  };
+  // per-item row offsets (fixed over K)
+  int64_t noff[NI], moff[MI];
+  bool nok[NI], mok[MI];
 #pragma unroll
-  for (int t = 0; t < KK; ++t) acc[t] = 0.f;
-  for (int e = beg + threadIdx.x; e < end; e += kT) {
-    const int oy = e / wo, ox = e - oy * wo;
-    const float gv = gp[e];
-    int ix[K];
-#pragma unroll
-    for (int kx = 0; kx < K; ++kx) ix[kx] = refl(ox * S - P + kx, wd);
-#pragma unroll
-    for (int ky = 0; ky < K; ++ky) {
-      const float* row = xp + refl(oy * S - P + ky, h) * wd;
-#pragma unroll
-      for (int kx = 0; kx < K; ++kx) acc[ky * K + kx] = fmaf(gv, row[ix[kx]], acc[ky * K + kx]);
+  for (int i = 0; i < NI; ++i) {
+    const int n = n0 + (tid + i * kT) % BN;
+    nok[i] = n < a.N;
+    if (a.foldN) {
+      const int bb = n / a.foldN;
+      noff[i] = bb * a.sBb + (int64_t)(n - bb * a.foldN) * a.sBn;
+    } else {
+      noff[i] = (int64_t)n * a.sBn;
     }
   }
 #pragma unroll
-  for (int t = 0; t < KK; ++t) {
-    float v = acc[t];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    acc[t] = v;
+  for (int i = 0; i < MI; ++i) {
+    const int m = m0 + (tid + i * kT) % BM;
+    mok[i] = m < a.M;
+    moff[i] = (int64_t)m * a.sAm;
   }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
+  float rn[NI][8], rm[MI][8];
+  auto load8 = [&](const float* base, bool ok, int kf, int64_t sK, bool vec, float* v) {
+    if (ok && vec && kf + 8 <= kend) {
+      const f32x4 u0 = *(const f32x4*)base, u1 = *(const f32x4*)(base + 4);
 #pragma unroll
-    for (int t = 0; t < KK; ++t) sh[wave][t] = acc[t];
+      for (int j = 0; j < 4; ++j) {
+        v[j] = u0[j];
+        v[4 + j] = u1[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (ok && kf + j < kend) ? base[j * sK] : 0.f;
+    }
+  };
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int kf = k0 + 8 * ((tid + i * kT) / BN);
+      const float* p = B + noff[i] + (kf < kend ? koffB(kf) : 0);
+      load8(p, nok[i], kf, a.sBk, f.vecB, rn[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int kf = k0 + 8 * ((tid + i * kT) / BM);
+      const float* p = A + moff[i] + (kf < kend ? koffA(kf) : 0);
+      load8(p, mok[i], kf, a.sAk, f.vecA, rm[i]);
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int it = tid + i * kT, row = it % BN, kg = it / BN;
+      bf16x8 t0, t1, t2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bf16 h, md, l;
+        ast_x3::split3(rn[i][j], h, md, l);
+        t0[j] = h;
+        t1[j] = md;
+        t2[j] = l;
+      }
+      *(bf16x8*)&Ns[0][row][8 * kg] = t0;
+      *(bf16x8*)&Ns[1][row][8 * kg] = t1;
+      *(bf16x8*)&Ns[2][row][8 * kg] = t2;
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int it = tid + i * kT, row = it % BM, kg = it / BM;
+      bf16x8 t0, t1, t2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bf16 h, md, l;
+        ast_x3::split3(rm[i][j], h, md, l);
+        t0[j] = h;
+        t1[j] = md;
+        t2[j] = l;
+      }
+      *(bf16x8*)&Ms[0][row][8 * kg] = t0;
+      *(bf16x8*)&Ms[1][row][8 * kg] = t1;
+      *(bf16x8*)&Ms[2][row][8 * kg] = t2;
+    }
+  };
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, r16 = lane & 15;
+  const bool first = g < 2;
+  if (kbeg < kend) load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += X3KC) {
+    __syncthreads();  // the previous chunk's fragments are read
+    stage();
+    __syncthreads();
+    if (k0 + X3KC < kend) load(k0 + X3KC);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ko = s * 16 + 8 * (g & 1);
+      bf16x8 f1[TN], f2[TN], g1[TM], g2[TM], g3[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int row = wn * WN + i * 16 + r16;
+        f1[i] = *(const bf16x8*)&Ns[first ? 0 : 1][row][ko];
+        f2[i] = *(const bf16x8*)&Ns[first ? 0 : 2][row][ko];
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int row = wm * WM + j * 16 + r16;
+        g1[j] = *(const bf16x8*)&Ms[0][row][ko];
+        g2[j] = *(const bf16x8*)&Ms[first ? 1 : 0][row][ko];
+        g3[j] = *(const bf16x8*)&Ms[first ? 2 : 1][row][ko];
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          f32x4 c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[i], g3[j], c, 0, 0, 0);  // n_hi m_lo + n_mid m_mid
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[i], g2[j], c, 0, 0, 0);  // n_hi m_mid + n_lo m_hi
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[i], g1[j], c, 0, 0, 0);  // n_hi m_hi + n_mid m_hi
+        }
+    }
   }
-  __syncthreads();
-  if (threadIdx.x < KK) {
-    const int t = threadIdx.x;
-    const int64_t row = ((int64_t)ch * gridDim.y + n) * gridDim.x + blockIdx.x;
-    part[row * KK + t] = (sh[0][t] + sh[1][t]) + (sh[2][t] + sh[3][t]);
+  // epilogue: lane holds D[n = 4 (lane >> 4) + r][m = lane & 15] of each 16 x 16 tile
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = n0 + wn * WN + i * 16 + 4 * g;
+    if (n >= a.N) continue;
+    const bool full = n + 3 < a.N;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * WM + j * 16 + r16;
+      if (m >= a.M) continue;
+      const f32x4 v = acc[i][j];
+      if (a.part) {
+        float* P = a.part + ((int64_t)blockIdx.z * a.M + m) * a.N + n;
+        if (full && f.vecP) {
+          *(f32x4*)P = v;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < a.N) P[r] = v[r];
+        }
+        continue;
+      }
+      if (full && f.vecC) {  // 4 consecutive n in one image, n-contiguous and aligned (host-checked)
+        int64_t ccol;
+        if (a.foldN) {
+          const int bb = n / a.foldN;
+          ccol = bb * a.sCb + (int64_t)(n - bb * a.foldN);
+        } else {
+          ccol = b * a.sCb + n;
+        }
+        f32x4* c = (f32x4*)(a.C + ccol + (int64_t)m * a.sCm);
+        *c = a.accumulate ? *c + v : v;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nn = n + r;
+          if (nn >= a.N) break;
+          int64_t ccol;
+          if (a.foldN) {
+            const int bb = nn / a.foldN;
+            ccol = bb * a.sCb + (int64_t)(nn - bb * a.foldN) * a.sCn;
+          } else {
+            ccol = b * a.sCb + (int64_t)nn * a.sCn;
+          }
+          float* c = a.C + ccol + (int64_t)m * a.sCm;
+          *c = a.accumulate ? *c + v[r] : v[r];
+        }
+      }
+    }
   }
 }
 
@@ -764,64 +826,30 @@ int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int
              ksplit, 0, accumulate, foldK, foldN};
   a.kchunk = ((K + ksplit - 1) / ksplit + GK - 1) / GK * GK;
   hipStream_t st = (hipStream_t)stream;
+  static const int x3 = [] {  // AST_MBGEMM_X3=0: the fp32-MFMA kernel for every shape (A/B runs)
+    const char* v = getenv("AST_MBGEMM_X3");
+    return v ? atoi(v) : 1;
+  }();
   const dim3 grid((unsigned)((N + GT - 1) / GT), (unsigned)((M + GT - 1) / GT), (unsigned)(batch * ksplit));
-  hipLaunchKernelGGL(gemm_kernel, grid, dim3(kT), 0, st, a);
+  if (x3 && (foldK == 0 || foldK % 8 == 0)) {  // split-bf16 path (8 consecutive k stay in one image)
+    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    X3Flags fl{};
+    fl.vecA = sAk == 1 && al(A) && sAm % 4 == 0 && (sAb % 4 == 0 || (batch == 1 && !foldK));
+    fl.vecB = sBk == 1 && al(B) && sBn % 4 == 0 && (sBb % 4 == 0 || (batch == 1 && !foldK && !foldN));
+    fl.vecC = sCn == 1 && al(C) && sCm % 4 == 0 && (sCb % 4 == 0 || (batch == 1 && !foldN)) &&
+              (foldN ? foldN % 4 == 0 : true);
+    fl.vecP = N % 4 == 0 && (need == 0 || al(workspace));
+    const dim3 gx((unsigned)((N + 127) / 128), (unsigned)((M + 63) / 64), (unsigned)(batch * ksplit));
+    hipLaunchKernelGGL((gemm_x3_kernel<64, 128>), gx, dim3(kT), 0, st, a, fl);
+  } else {
+    hipLaunchKernelGGL(gemm_kernel, grid, dim3(kT), 0, st, a);
+  }
   if (need > 0) {  // the partial tiles, summed in (image, split) order
     const bool shared = sCb == 0 && batch > 1;
     const int cimgs = shared ? 1 : batch;
     const int zper = shared ? batch * ksplit : ksplit;
     const int64_t mn = (int64_t)M * N;
     hipLaunchKernelGGL(gemm_reduce_kernel, dim3(grid_for(mn, 8192), (unsigned)cimgs), dim3(kT), 0, st, a, zper);
-  }
-  return (int)hipGetLastError();
-}
-
-#define AST_DW_DISPATCH(KERNEL, grid, ...)                                                          \
-  do {                                                                                              \
-    if (k == 3 && s == 1) hipLaunchKernelGGL((KERNEL<3, 1>), grid, dim3(kT), 0, st, __VA_ARGS__);   \
-    else if (k == 3) hipLaunchKernelGGL((KERNEL<3, 2>), grid, dim3(kT), 0, st, __VA_ARGS__);        \
-    else if (s == 1) hipLaunchKernelGGL((KERNEL<5, 1>), grid, dim3(kT), 0, st, __VA_ARGS__);        \
-    else hipLaunchKernelGGL((KERNEL<5, 2>), grid, dim3(kT), 0, st, __VA_ARGS__);                    \
-  } while (0)
-
-long long ast_mbt_dw_workspace_floats(int n, int c, int h, int wd, int k) {
-  if (n <= 0 || c <= 0 || h <= 0 || wd <= 0 || (k != 3 && k != 5)) return 0;
-  const long long dpad = (long long)n * c * (h + k - 1) * (wd + k - 1);            // mode 1
-  const long long wpart = (long long)c * n * ((h * wd + DW_SEG - 1) / DW_SEG) * k * k;  // mode 2 (stride 1 bound)
-  return dpad > wpart ? dpad : wpart;
-}
-
-int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, float* out, int n, int c, int h, int wd,
-                   int k, int s, float* workspace, long long workspace_floats, void* stream) {
-  if (!w || !out || (mode != 1 && !x) || (mode != 0 && !g) || (mode != 0 && !workspace)) return AST_E_NULLPTR;
-  if (n <= 0 || c <= 0 || h <= 0 || wd <= 0 || (k != 3 && k != 5) || (s != 1 && s != 2)) return AST_E_SHAPE;
-  const int p = (k - 1) / 2;
-  if (p >= h || p >= wd) return AST_E_SHAPE;  // reflect padding needs pad < size
-  const int ho = (h + 2 * p - k) / s + 1, wo = (wd + 2 * p - k) / s + 1;
-  const int64_t nc = (int64_t)n * c;
-  if (nc * (h + 2 * p) * (wd + 2 * p) >= (1LL << 31) || n > 65535 || c > 65535) return AST_E_SHAPE;  // 32-bit indices
-  hipStream_t st = (hipStream_t)stream;
-  const unsigned gy = (unsigned)(nc < 65535 ? nc : 65535);
-  if (mode == 0) {
-    AST_DW_DISPATCH(dw_fwd_kernel, dim3((ho * wo + kT - 1) / kT, gy), x, w, out, (int)nc, c, h, wd, ho, wo);
-  } else if (mode == 1) {
-    if (workspace_floats < ast_mbt_dw_workspace_floats(n, c, h, wd, k)) return AST_E_SHAPE;  // workspace too small
-    const int hp = h + 2 * p, wp = wd + 2 * p;
-    AST_DW_DISPATCH(dw_dpad_kernel, dim3((hp * wp + kT - 1) / kT, gy), g, w, workspace, (int)nc, c, hp, wp, ho, wo);
-    if (p == 1)
-      hipLaunchKernelGGL(dw_fold_kernel<1>, dim3((h * wd + kT - 1) / kT, gy), dim3(kT), 0, st, workspace, out, (int)nc,
-                         h, wd);
-    else
-      hipLaunchKernelGGL(dw_fold_kernel<2>, dim3((h * wd + kT - 1) / kT, gy), dim3(kT), 0, st, workspace, out, (int)nc,
-                         h, wd);
-  } else {
-    const int segs = (ho * wo + DW_SEG - 1) / DW_SEG;
-    const int64_t rows = (int64_t)n * segs;  // partials per channel: (image, segment) rows of k*k
-    if (workspace_floats < (long long)c * rows * k * k) return AST_E_SHAPE;  // workspace too small
-    const dim3 grid((unsigned)segs, (unsigned)n, (unsigned)c);
-    AST_DW_DISPATCH(dw_wgrad_kernel, grid, x, g, workspace, c, h, wd, ho, wo);
-    const hipError_t e = ast_det::reduce_cols(workspace, rows, k * k, k * k, c, rows * k * k, out, k * k, false, st);
-    if (e != hipSuccess) return (int)e;
   }
   return (int)hipGetLastError();
 }

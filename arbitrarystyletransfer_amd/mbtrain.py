@@ -126,10 +126,8 @@ class DwConvFn(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            ws = torch.empty((lib().ast_mbt_dw_workspace_floats(n, c, h, w, ctx.k),), device=x.device,
-                             dtype=torch.float32)
-            check(lib().ast_mbt_dw_f32(1, None, ptr(wt), ptr(g), ptr(dx), n, c, h, w, ctx.k, ctx.s, ptr(ws), ws.numel(),
-                                       _s(g)), "dw dgrad")
+            check(lib().ast_mbt_dw_f32(1, None, ptr(wt), ptr(g), ptr(dx), n, c, h, w, ctx.k, ctx.s, None, 0, _s(g)),
+                  "dw dgrad")
         if ctx.needs_input_grad[1]:
             dw = torch.empty((c, ctx.k * ctx.k), device=g.device, dtype=torch.float32)
             ws = workspace(lib().ast_mbt_dw_workspace_floats(n, c, h, w, ctx.k), x.device)

@@ -466,10 +466,11 @@ int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int
                      int accumulate, int foldK, int foldN, float* workspace, long long workspace_floats,
                      void* stream);
 
-/* Depthwise k x k conv (k 3|5, stride 1|2, reflect pad (k-1)/2; mobilenetv2.py:148-149, :116-117):
- * mode 0 out = conv(x, w); 1 out = dx from g (overwritten; the workspace holds the padded-input
- * gradient); 2 out = dw [c][k*k] from x, g (overwritten; the workspace holds the per-segment
- * partials). Modes 1 and 2 need ast_mbt_dw_workspace_floats floats of workspace. */
+/* Depthwise k x k conv (k 3|5, stride 1|2, reflect pad (k-1)/2; mobilenetv2.py:148-149, :116-117),
+ * LDS-tiled (csrc/mbt_dw.hip): mode 0 out = conv(x, w); 1 out = dx from g (overwritten, one pass,
+ * no workspace); 2 out = dw [c][k*k] from x, g (overwritten; the workspace holds one partial row
+ * per (channel, image, tile group), summed in that order). Mode 2 needs
+ * ast_mbt_dw_workspace_floats floats of workspace (modes 0 and 1 ignore it). */
 long long ast_mbt_dw_workspace_floats(int n, int c, int h, int wd, int k);
 int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, float* out, int n,
                    int c, int h, int wd, int k, int s, float* workspace, long long workspace_floats,

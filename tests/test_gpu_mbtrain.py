@@ -59,7 +59,11 @@ def test_pw_conv(split, shape, cout):
 
 
 @pytest.mark.parametrize("k,s,hw", [(3, 1, (10, 14)), (5, 1, (9, 12)), (3, 2, (11, 16)), (5, 2, (12, 9)), (5, 1, (3, 4)),
-                                    (3, 2, (2, 3)), (5, 2, (50, 47)), (3, 1, (48, 50))])
+                                    (3, 2, (2, 3)), (5, 2, (50, 47)), (3, 1, (48, 50)),
+                                    # the LDS-tiled kernels' tile shapes (csrc/mbt_dw.hip dw_plan): full
+                                    # 160^2 planes, partial tiles in both axes, multi-tile wgrad groups
+                                    (5, 1, (160, 160)), (3, 1, (80, 83)), (5, 2, (81, 80)), (3, 2, (40, 40)),
+                                    (5, 1, (20, 20)), (3, 1, (131, 67))])
 def test_dw_conv(k, s, hw):
     torch.manual_seed(1)
     c = 12
