@@ -225,7 +225,22 @@ constexpr int X3KC = 32, X3KP = X3KC + 8;
 
 struct X3Flags {
   int vecA, vecB, vecC, vecP;  // 16-byte paths legal: A / B k-runs, C / partial-tile n-runs
+  int ntn;                     // n-tiles; a workgroup walks n-tiles blockIdx.x, + gridDim.x, ...
 };
+
+// Staging map of one operand side with R rows: item it -> (row, 8-k group). When k is the
+// contiguous dimension, 4 consecutive lanes take the 4 groups of one row (128-byte runs per row);
+// otherwise consecutive lanes take consecutive rows (every k load coalesced across the lanes).
+template <int R>
+__device__ __forceinline__ void x3_item(int it, bool kfast, int& row, int& kg) {
+  if (kfast) {
+    row = it >> 2;
+    kg = it & 3;
+  } else {
+    row = it % R;
+    kg = it / R;
+  }
+}
 
 template <int BM, int BN>
 __global__ __launch_bounds__(kT, 2) void gemm_x3_kernel(GemmArgs a, X3Flags f) {
@@ -239,9 +254,11 @@ __global__ __launch_bounds__(kT, 2) void gemm_x3_kernel(GemmArgs a, X3Flags f) {
   static_assert(NI >= 1 && MI >= 1 && BN * 4 % kT == 0 && BM * 4 % kT == 0, "tile");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave & 1, wm = wave >> 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int m0 = blockIdx.y * BM;
   const int b = blockIdx.z / a.ksplit, ks = blockIdx.z % a.ksplit;
   const int kbeg = ks * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
+  if ((int)blockIdx.x >= f.ntn) return;  // (an empty K split still stores its zero tiles)
+  const bool kfA = a.sAk == 1, kfB = a.sBk == 1;
   const float* A = a.A + b * a.sAb;
   const float* B = a.B + b * a.sBb;
   // k offsets: folded K walks images through the batch stride (batch == 1 then)
@@ -259,23 +276,28 @@ __global__ __launch_bounds__(kT, 2) void gemm_x3_kernel(GemmArgs a, X3Flags f) {
     }
     return (int64_t)k * a.sBk;
   };
-  // per-item row offsets (fixed over K)
   int64_t noff[NI], moff[MI];
   bool nok[NI], mok[MI];
+  auto set_ntile = [&](int t) {  // per-item column offsets of n-tile t
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int n = n0 + (tid + i * kT) % BN;
-    nok[i] = n < a.N;
-    if (a.foldN) {
-      const int bb = n / a.foldN;
-      noff[i] = bb * a.sBb + (int64_t)(n - bb * a.foldN) * a.sBn;
-    } else {
-      noff[i] = (int64_t)n * a.sBn;
+    for (int i = 0; i < NI; ++i) {
+      int row, kg;
+      x3_item<BN>(tid + i * kT, kfB, row, kg);
+      const int n = t * BN + row;
+      nok[i] = n < a.N;
+      if (a.foldN) {
+        const int bb = n / a.foldN;
+        noff[i] = bb * a.sBb + (int64_t)(n - bb * a.foldN) * a.sBn;
+      } else {
+        noff[i] = (int64_t)n * a.sBn;
+      }
     }
-  }
+  };
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
-    const int m = m0 + (tid + i * kT) % BM;
+    int row, kg;
+    x3_item<BM>(tid + i * kT, kfA, row, kg);
+    const int m = m0 + row;
     mok[i] = m < a.M;
     moff[i] = (int64_t)m * a.sAm;
   }
@@ -296,49 +318,47 @@ __global__ __launch_bounds__(kT, 2) void gemm_x3_kernel(GemmArgs a, X3Flags f) {
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int kf = k0 + 8 * ((tid + i * kT) / BN);
+      int row, kg;
+      x3_item<BN>(tid + i * kT, kfB, row, kg);
+      const int kf = k0 + 8 * kg;
       const float* p = B + noff[i] + (kf < kend ? koffB(kf) : 0);
       load8(p, nok[i], kf, a.sBk, f.vecB, rn[i]);
     }
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
-      const int kf = k0 + 8 * ((tid + i * kT) / BM);
+      int row, kg;
+      x3_item<BM>(tid + i * kT, kfA, row, kg);
+      const int kf = k0 + 8 * kg;
       const float* p = A + moff[i] + (kf < kend ? koffA(kf) : 0);
       load8(p, mok[i], kf, a.sAk, f.vecA, rm[i]);
     }
   };
+  auto split_store = [&](const float* v, bf16* d0, bf16* d1, bf16* d2) {
+    bf16x8 t0, t1, t2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bf16 h, md, l;
+      ast_x3::split3(v[j], h, md, l);
+      t0[j] = h;
+      t1[j] = md;
+      t2[j] = l;
+    }
+    *(bf16x8*)d0 = t0;
+    *(bf16x8*)d1 = t1;
+    *(bf16x8*)d2 = t2;
+  };
   auto stage = [&]() {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int it = tid + i * kT, row = it % BN, kg = it / BN;
-      bf16x8 t0, t1, t2;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        bf16 h, md, l;
-        ast_x3::split3(rn[i][j], h, md, l);
-        t0[j] = h;
-        t1[j] = md;
-        t2[j] = l;
-      }
-      *(bf16x8*)&Ns[0][row][8 * kg] = t0;
-      *(bf16x8*)&Ns[1][row][8 * kg] = t1;
-      *(bf16x8*)&Ns[2][row][8 * kg] = t2;
+      int row, kg;
+      x3_item<BN>(tid + i * kT, kfB, row, kg);
+      split_store(rn[i], &Ns[0][row][8 * kg], &Ns[1][row][8 * kg], &Ns[2][row][8 * kg]);
     }
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
-      const int it = tid + i * kT, row = it % BM, kg = it / BM;
-      bf16x8 t0, t1, t2;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        bf16 h, md, l;
-        ast_x3::split3(rm[i][j], h, md, l);
-        t0[j] = h;
-        t1[j] = md;
-        t2[j] = l;
-      }
-      *(bf16x8*)&Ms[0][row][8 * kg] = t0;
-      *(bf16x8*)&Ms[1][row][8 * kg] = t1;
-      *(bf16x8*)&Ms[2][row][8 * kg] = t2;
+      int row, kg;
+      x3_item<BM>(tid + i * kT, kfA, row, kg);
+      split_store(rm[i], &Ms[0][row][8 * kg], &Ms[1][row][8 * kg], &Ms[2][row][8 * kg]);
     }
   };
   f32x4 acc[TN][TM];
@@ -348,12 +368,77 @@ __global__ __launch_bounds__(kT, 2) void gemm_x3_kernel(GemmArgs a, X3Flags f) {
     for (int j = 0; j < TM; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, r16 = lane & 15;
   const bool first = g < 2;
-  if (kbeg < kend) load(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += X3KC) {
+  // epilogue of n-tile t: lane holds D[n = 4 (lane >> 4) + r][m = lane & 15] of each 16 x 16 tile
+  auto epilogue = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = t * BN + wn * WN + i * 16 + 4 * g;
+      if (n >= a.N) continue;
+      const bool full = n + 3 < a.N;
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0 + wm * WM + j * 16 + r16;
+        if (m >= a.M) continue;
+        const f32x4 v = acc[i][j];
+        if (a.part) {
+          float* P = a.part + ((int64_t)blockIdx.z * a.M + m) * a.N + n;
+          if (full && f.vecP) {
+            *(f32x4*)P = v;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < a.N) P[r] = v[r];
+          }
+          continue;
+        }
+        if (full && f.vecC) {  // 4 consecutive n in one image, n-contiguous and aligned (host-checked)
+          int64_t ccol;
+          if (a.foldN) {
+            const int bb = n / a.foldN;
+            ccol = bb * a.sCb + (int64_t)(n - bb * a.foldN);
+          } else {
+            ccol = b * a.sCb + n;
+          }
+          f32x4* c = (f32x4*)(a.C + ccol + (int64_t)m * a.sCm);
+          *c = a.accumulate ? *c + v : v;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int nn = n + r;
+            if (nn >= a.N) break;
+            int64_t ccol;
+            if (a.foldN) {
+              const int bb = nn / a.foldN;
+              ccol = bb * a.sCb + (int64_t)(nn - bb * a.foldN) * a.sCn;
+            } else {
+              ccol = b * a.sCb + (int64_t)nn * a.sCn;
+            }
+            float* c = a.C + ccol + (int64_t)m * a.sCm;
+            *c = a.accumulate ? *c + v[r] : v[r];
+          }
+        }
+      }
+    }
+  };
+  // (n-tile, K chunk) pairs in one pipelined walk: the next pair's loads (the next tile's first
+  // chunk after a tile's last) are in flight during this pair's MFMAs and the tile's epilogue
+  int t = blockIdx.x, k0 = kbeg;
+  set_ntile(t);
+  load(k0);
+  for (;;) {
     __syncthreads();  // the previous chunk's fragments are read
     stage();
     __syncthreads();
-    if (k0 + X3KC < kend) load(k0 + X3KC);
+    int nt = t, nk = k0 + X3KC;
+    if (nk >= kend) {
+      nt = t + gridDim.x;
+      nk = kbeg;
+    }
+    const bool more = nt < f.ntn;
+    if (more) {
+      if (nt != t) set_ntile(nt);
+      load(nk);
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int ko = s * 16 + 8 * (g & 1);
@@ -381,56 +466,16 @@ __global__ __launch_bounds__(kT, 2) void gemm_x3_kernel(GemmArgs a, X3Flags f) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[i], g1[j], c, 0, 0, 0);  // n_hi m_hi + n_mid m_hi
         }
     }
-  }
-  // epilogue: lane holds D[n = 4 (lane >> 4) + r][m = lane & 15] of each 16 x 16 tile
+    if (k0 + X3KC >= kend) {  // the tile's last chunk: store and restart the accumulators
+      epilogue(t);
 #pragma unroll
-  for (int i = 0; i < TN; ++i) {
-    const int n = n0 + wn * WN + i * 16 + 4 * g;
-    if (n >= a.N) continue;
-    const bool full = n + 3 < a.N;
+      for (int i = 0; i < TN; ++i)
 #pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int m = m0 + wm * WM + j * 16 + r16;
-      if (m >= a.M) continue;
-      const f32x4 v = acc[i][j];
-      if (a.part) {
-        float* P = a.part + ((int64_t)blockIdx.z * a.M + m) * a.N + n;
-        if (full && f.vecP) {
-          *(f32x4*)P = v;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < a.N) P[r] = v[r];
-        }
-        continue;
-      }
-      if (full && f.vecC) {  // 4 consecutive n in one image, n-contiguous and aligned (host-checked)
-        int64_t ccol;
-        if (a.foldN) {
-          const int bb = n / a.foldN;
-          ccol = bb * a.sCb + (int64_t)(n - bb * a.foldN);
-        } else {
-          ccol = b * a.sCb + n;
-        }
-        f32x4* c = (f32x4*)(a.C + ccol + (int64_t)m * a.sCm);
-        *c = a.accumulate ? *c + v : v;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int nn = n + r;
-          if (nn >= a.N) break;
-          int64_t ccol;
-          if (a.foldN) {
-            const int bb = nn / a.foldN;
-            ccol = bb * a.sCb + (int64_t)(nn - bb * a.foldN) * a.sCn;
-          } else {
-            ccol = b * a.sCb + (int64_t)nn * a.sCn;
-          }
-          float* c = a.C + ccol + (int64_t)m * a.sCm;
-          *c = a.accumulate ? *c + v[r] : v[r];
-        }
-      }
+        for (int j = 0; j < TM; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
+    if (!more) break;
+    t = nt;
+    k0 = nk;
   }
 }
 
@@ -826,9 +871,11 @@ int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int
              ksplit, 0, accumulate, foldK, foldN};
   a.kchunk = ((K + ksplit - 1) / ksplit + GK - 1) / GK * GK;
   hipStream_t st = (hipStream_t)stream;
-  static const int x3 = [] {  // AST_MBGEMM_X3=0: the fp32-MFMA kernel for every shape (A/B runs)
+  // AST_MBGEMM_X3=1: the split-bf16 kernel (fp32-level accuracy, repeatable; measured 3% slower
+  // on the AST step than the fp32-MFMA kernel, whose skinny-K shapes are latency-, not MFMA-bound)
+  static const int x3 = [] {
     const char* v = getenv("AST_MBGEMM_X3");
-    return v ? atoi(v) : 1;
+    return v ? atoi(v) : 0;
   }();
   const dim3 grid((unsigned)((N + GT - 1) / GT), (unsigned)((M + GT - 1) / GT), (unsigned)(batch * ksplit));
   if (x3 && (foldK == 0 || foldK % 8 == 0)) {  // split-bf16 path (8 consecutive k stay in one image)
@@ -839,7 +886,11 @@ int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int
     fl.vecC = sCn == 1 && al(C) && sCm % 4 == 0 && (sCb % 4 == 0 || (batch == 1 && !foldN)) &&
               (foldN ? foldN % 4 == 0 : true);
     fl.vecP = N % 4 == 0 && (need == 0 || al(workspace));
-    const dim3 gx((unsigned)((N + 127) / 128), (unsigned)((M + 63) / 64), (unsigned)(batch * ksplit));
+    // n-tiles walked by a grid of ~2 resident workgroups per CU (pipelined across tiles)
+    fl.ntn = (N + 127) / 128;
+    const int mt = (M + 63) / 64, zb = batch * ksplit;
+    const int want = (int)((512 + (int64_t)mt * zb - 1) / ((int64_t)mt * zb));
+    const dim3 gx((unsigned)(want < fl.ntn ? want : fl.ntn), (unsigned)mt, (unsigned)zb);
     hipLaunchKernelGGL((gemm_x3_kernel<64, 128>), gx, dim3(kT), 0, st, a, fl);
   } else {
     hipLaunchKernelGGL(gemm_kernel, grid, dim3(kT), 0, st, a);

@@ -39,6 +39,8 @@ class AdaIN(nn.Module):
         self.canonical = canonical
 
     def forward(self, content_map, style_map, alpha: float = 1.0):
+        if _compiling():   # torch.compile: the registered op (fake impl + autograd), no graph break
+            return torch.ops.ast_hip.adain_map(content_map, style_map, float(alpha), not self.canonical)
         if torch.is_grad_enabled() and (content_map.requires_grad or style_map.requires_grad):
             return Fn.AdaINFn.apply(content_map, style_map, float(alpha), not self.canonical)
         return ops.adain(content_map, style_map, alpha=alpha, swap_style_stats=not self.canonical)
@@ -87,6 +89,19 @@ class AdaAttN(nn.Module):
             from . import attention
             return attention.adaattn(self, content_map, style_map)
         return ops.adaattn(content_map, style_map, self.W_q.weight, self.W_k.weight, self.W_v.weight)
+
+
+def _compiling() -> bool:
+    """Under torch.compile / dynamo tracing the modules call torch.ops.ast_hip.* (library.py: the
+    same C-ABI kernels behind registered custom ops with fake implementations) and pack weights
+    with the ast_hip::conv3x3_pack op instead of the data_ptr-keyed caches, which dynamo cannot
+    trace. Eager calls keep the direct C-ABI launches (no dispatcher overhead per launch)."""
+    return torch.compiler.is_compiling()
+
+
+def _ops():
+    from . import library  # noqa: F401  (registers the ast_hip::* custom ops)
+    return torch.ops.ast_hip
 
 
 def _needs_grad(x, module):
@@ -212,6 +227,8 @@ class PretrainedEncoder(nn.Module):
         """Feature maps of the requested layers. `x2` (optional, same C/H/W): a second batch
         encoded in the same launches, outputs hold x's images then x2's."""
         norm = self._vgg_layers[0]
+        if _compiling():
+            return self._forward_ops(x, x2)
         if _needs_grad(x, self) or (x2 is not None and _needs_grad(x2, self)):
             if x2 is not None:
                 return [torch.cat(p) for p in zip(self._forward_autograd(x), self._forward_autograd(x2))]
@@ -224,6 +241,24 @@ class PretrainedEncoder(nn.Module):
                 cur, self._packed.get(conv), conv.bias, conv.out_channels, pad_mode="zeros",
                 in_mean=norm.mean.view(-1) if first else None, in_std=norm.std.view(-1) if first else None,
                 want_pre=want_pre, want_act=want_act, want_pool=want_pool, x2=cur2)
+            by_name = {conv.name: pre, f"relu_{idx}": act, f"pool_{idx}": pool}
+            outs.extend(by_name[nm] for nm in collect)
+            cur, cur2 = (pool if want_pool else act), None
+        return outs
+
+    def _forward_ops(self, x, x2=None):
+        """The same walk through torch.ops.ast_hip.conv3x3 (torch.compile path; with autograd its
+        registered backward runs the same HIP dgrad / wgrad kernels)."""
+        A = _ops()
+        norm = self._vgg_layers[0]
+        outs = []
+        cur, cur2 = x, x2
+        grad = x2 is None and _needs_grad(x, self)
+        for idx, conv, want_pre, want_act, want_pool, collect in self._plan():
+            first = idx == 1
+            pre, act, pool = A.conv3x3(cur, conv.weight, A.conv3x3_pack(conv.weight.detach()), conv.bias, 1, 0,
+                                       norm.mean.view(-1) if first else None, norm.std.view(-1) if first else None,
+                                       want_pre or grad, want_act, want_pool, cur2)
             by_name = {conv.name: pre, f"relu_{idx}": act, f"pool_{idx}": pool}
             outs.extend(by_name[nm] for nm in collect)
             cur, cur2 = (pool if want_pool else act), None
@@ -297,6 +332,13 @@ class VGGDecoder(nn.Sequential):
             conv.bias.copy_(torch.from_numpy(b))
 
     def forward(self, x):
+        if _compiling():
+            A = _ops()
+            for conv, up, relu in self._groups:
+                pre, act, _ = A.conv3x3(x, conv.weight, A.conv3x3_pack(conv.weight.detach()), conv.bias,
+                                        2 if up else 1, 1, None, None, not relu, relu, False, None)
+                x = act if relu else pre
+            return x
         if _needs_grad(x, self):
             for conv, up, relu in self._groups:
                 x = Fn.DecoderConvFn.apply(x, conv.weight, conv.bias, self._packed.get(conv), 2 if up else 1, relu)
