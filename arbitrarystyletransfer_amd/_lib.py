@@ -97,6 +97,7 @@ SIGNATURES = {
                               _ll, _p]),
     "ast_mbt_dw_workspace_floats": (_ll, [_i, _i, _i, _i, _i]),
     "ast_mbt_dw_f32": (_i, [_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _ll, _p]),
+    "ast_mbt_dw_act_f32": (_i, [_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _ll, _p]),
     "ast_mbt_bn_workspace_floats": (_ll, [_i, _i, _ll]),
     "ast_mbt_bn_fwd_f32": (_i, [_p, _i, _i, _ll, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _ll, _p]),
     "ast_mbt_bn_bwd_f32": (_i, [_p, _p, _i, _i, _ll, _p, _p, _p, _p, _p, _p, _p, _ll, _p]),
@@ -105,8 +106,14 @@ SIGNATURES = {
     "ast_mbt_bn_apply_f32": (_i, [_p, _i, _i, _ll, _p, _p, _p, _p, _p, _p]),
     "ast_mbt_bn_bwd_sums_f32": (_i, [_p, _p, _i, _i, _ll, _p, _p, _p, _ll, _p, _p]),
     "ast_mbt_bn_bwd_apply_f32": (_i, [_p, _p, _i, _i, _ll, _p, _p, _p, _p, _p, _p, _p]),
+    "ast_mbt_bn_act_fwd_f32": (_i, [_p, _i, _i, _ll, _p, _p, _f, _f, _p, _p, _p, _p, _i, _p, _p, _ll, _p]),
+    "ast_mbt_bn_act_apply_f32": (_i, [_p, _i, _i, _ll, _p, _p, _p, _p, _i, _p, _p]),
+    "ast_mbt_bn_act_bwd_f32": (_i, [_p, _p, _i, _i, _ll, _p, _p, _p, _p, _i, _p, _p, _p, _p, _ll, _p]),
+    "ast_mbt_bn_act_bwd_sums_f32": (_i, [_p, _p, _i, _i, _ll, _p, _p, _p, _p, _i, _p, _ll, _p, _p]),
+    "ast_mbt_bn_act_bwd_apply_f32": (_i, [_p, _p, _i, _i, _ll, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "ast_mbt_eltwise_f32": (_i, [_i, _p, _p, _p, _ll, _i, _i, _p]),
     "ast_mbt_plane_f32": (_i, [_i, _p, _p, _p, _p, _p, _ll, _ll, _p]),
+    "ast_mbt_plane_act_f32": (_i, [_i, _p, _p, _p, _p, _p, _p, _ll, _ll, _p]),
     "ast_mbt_se_fc_fwd_f32": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p]),
     "ast_mbt_se_fc_bwd_f32": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _ll, _p, _p, _p, _p, _p, _p, _ll, _p]),
 }

@@ -39,19 +39,29 @@ struct Geo {
   static constexpr int SR = (R - 1) * S + K;                 // input rows one strip reads
 };
 
-// stage x[plane] rows iy0.., cols ix0.. (reflected) into xs[IH][IWP]
+// Hardswish and its derivative (torch's formulas; the expressions of mbtrain.hip's elt<0> / elt<1>,
+// so a fused activation is bit-identical to the materialised one)
+__device__ __forceinline__ float hswish(float a) { return a * fminf(fmaxf(a + 3.f, 0.f), 6.f) / 6.f; }
+__device__ __forceinline__ float hswish_bwd(float a, float g) {
+  return a < -3.f ? 0.f : (a <= 3.f ? g * (a / 3.f + 0.5f) : g);
+}
+
+// stage x[plane] rows iy0.., cols ix0.. (reflected) into xs[IH][IWP]; act: the conv's input is
+// hardswish(x) (DepthWiseConv's Hardswish -> depthwise conv, mobilenetv2.py:144-149, fused)
 template <class G>
-__device__ __forceinline__ void stage_input(float* xs, const float* __restrict__ xp, int iy0, int ix0, int h, int wd) {
+__device__ __forceinline__ void stage_input(float* xs, const float* __restrict__ xp, int iy0, int ix0, int h, int wd,
+                                            bool act) {
   for (int e = threadIdx.x; e < G::IH * G::IW; e += kT) {
     const int r = e / G::IW, c = e - r * G::IW;
-    xs[r * G::IWP + c] = xp[reflc(iy0 + r, h) * wd + reflc(ix0 + c, wd)];
+    const float v = xp[reflc(iy0 + r, h) * wd + reflc(ix0 + c, wd)];
+    xs[r * G::IWP + c] = act ? hswish(v) : v;
   }
 }
 
 template <int K, int S, int TW, int R>
 __global__ __launch_bounds__(kT) void dwt_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                      float* __restrict__ y, int planes, int c, int h, int wd, int ho,
-                                                     int wo, int tiles_x) {
+                                                     int wo, int tiles_x, int act) {
   using G = Geo<K, S, TW, R>;
   __shared__ float xs[G::IH * G::IWP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -64,7 +74,7 @@ __global__ __launch_bounds__(kT) void dwt_fwd_kernel(const float* __restrict__ x
 #pragma unroll
     for (int t = 0; t < G::KK; ++t) wr[t] = wc[t];
     __syncthreads();  // the previous plane's window is consumed
-    stage_input<G>(xs, x + (int64_t)pl * h * wd, oy0 * S - G::P, ox0 * S - G::P, h, wd);
+    stage_input<G>(xs, x + (int64_t)pl * h * wd, oy0 * S - G::P, ox0 * S - G::P, h, wd, act != 0);
     __syncthreads();
     float acc[R];
 #pragma unroll
@@ -110,8 +120,9 @@ __device__ __forceinline__ int floor_div2(int a) { return a >> 1; }  // arithmet
 
 template <int K, int S, int TW, int R>
 __global__ __launch_bounds__(kT) void dwt_dgrad_kernel(const float* __restrict__ g, const float* __restrict__ w,
-                                                       float* __restrict__ dx, int planes, int c, int h, int wd,
-                                                       int ho, int wo, int tiles_x) {
+                                                       const float* __restrict__ xa, float* __restrict__ dx,
+                                                       int planes, int c, int h, int wd, int ho, int wo,
+                                                       int tiles_x) {
   using G = Geo<K, S, TW, R>;
   using D = DGeo<K, S, TW, R>;
   constexpr int P = G::P;
@@ -211,7 +222,8 @@ __global__ __launch_bounds__(kT) void dwt_dgrad_kernel(const float* __restrict__
         if (cx1 >= 0) acc += ds[ry2 * D::QWP + cx1];
         if (cx2 >= 0) acc += ds[ry2 * D::QWP + cx2];
       }
-      dxp[iy * wd + ix] = acc;
+      // xa: the conv input was hardswish(xa): the gradient continues through it
+      dxp[iy * wd + ix] = xa ? hswish_bwd(xa[(int64_t)pl * h * wd + iy * wd + ix], acc) : acc;
     }
   }
 }
@@ -220,7 +232,7 @@ __global__ __launch_bounds__(kT) void dwt_dgrad_kernel(const float* __restrict__
 template <int K, int S, int TW, int R>
 __global__ __launch_bounds__(kT) void dwt_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                        float* __restrict__ part, int c, int h, int wd, int ho, int wo,
-                                                       int tiles_x, int ntiles, int tpb) {
+                                                       int tiles_x, int ntiles, int tpb, int act) {
   using G = Geo<K, S, TW, R>;
   constexpr int KK = G::KK;
   __shared__ float xs[G::IH * G::IWP];
@@ -239,7 +251,7 @@ __global__ __launch_bounds__(kT) void dwt_wgrad_kernel(const float* __restrict__
     const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
     const int oy0 = ty * G::TH, ox0 = tx * TW, ox = ox0 + lx;
     __syncthreads();
-    stage_input<G>(xs, xp, oy0 * S - G::P, ox0 * S - G::P, h, wd);
+    stage_input<G>(xs, xp, oy0 * S - G::P, ox0 * S - G::P, h, wd, act != 0);
     float gv[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -336,7 +348,7 @@ void dw_launch(int k, int s, const DwPlan& p, A... args) {
 struct DwArgs {
   const float *x, *w, *g;
   float *out, *part;
-  int n, c, h, wd, ho, wo, groups;
+  int n, c, h, wd, ho, wo, groups, act;
   DwPlan p;
   hipStream_t st;
 };
@@ -347,7 +359,7 @@ struct FwdL {
     const int64_t nc = (int64_t)a.n * a.c;
     const dim3 grid((unsigned)(a.p.tiles_x * a.p.tiles_y), (unsigned)(nc < 65535 ? nc : 65535));
     hipLaunchKernelGGL((dwt_fwd_kernel<K, S, TW, R>), grid, dim3(kT), 0, a.st, a.x, a.w, a.out, (int)nc, a.c, a.h, a.wd,
-                       a.ho, a.wo, a.p.tiles_x);
+                       a.ho, a.wo, a.p.tiles_x, a.act);
   }
 };
 
@@ -356,8 +368,8 @@ struct DgradL {
   static void run(const DwArgs& a) {
     const int64_t nc = (int64_t)a.n * a.c;
     const dim3 grid((unsigned)(a.p.tiles_x * a.p.tiles_y), (unsigned)(nc < 65535 ? nc : 65535));
-    hipLaunchKernelGGL((dwt_dgrad_kernel<K, S, TW, R>), grid, dim3(kT), 0, a.st, a.g, a.w, a.out, (int)nc, a.c, a.h,
-                       a.wd, a.ho, a.wo, a.p.tiles_x);
+    hipLaunchKernelGGL((dwt_dgrad_kernel<K, S, TW, R>), grid, dim3(kT), 0, a.st, a.g, a.w, a.act ? a.x : nullptr, a.out,
+                       (int)nc, a.c, a.h, a.wd, a.ho, a.wo, a.p.tiles_x);
   }
 };
 
@@ -366,7 +378,7 @@ struct WgradL {
   static void run(const DwArgs& a) {
     const dim3 grid((unsigned)a.groups, (unsigned)a.n, (unsigned)a.c);
     hipLaunchKernelGGL((dwt_wgrad_kernel<K, S, TW, R>), grid, dim3(kT), 0, a.st, a.x, a.g, a.part, a.c, a.h, a.wd,
-                       a.ho, a.wo, a.p.tiles_x, a.p.tiles_x * a.p.tiles_y, kTpb);
+                       a.ho, a.wo, a.p.tiles_x, a.p.tiles_x * a.p.tiles_y, kTpb, a.act);
   }
 };
 
@@ -387,9 +399,11 @@ long long ast_mbt_dw_workspace_floats(int n, int c, int h, int wd, int k) {
   return (long long)c * n * groups * k * k;
 }
 
-int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, float* out, int n, int c, int h, int wd,
-                   int k, int s, float* workspace, long long workspace_floats, void* stream) {
-  if (!w || !out || (mode != 1 && !x) || (mode != 0 && !g) || (mode == 2 && !workspace)) return AST_E_NULLPTR;
+int ast_mbt_dw_act_f32(int mode, const float* x, const float* w, const float* g, float* out, int n, int c, int h,
+                       int wd, int k, int s, int act, float* workspace, long long workspace_floats, void* stream) {
+  if (!w || !out || ((mode != 1 || act) && !x) || (mode != 0 && !g) || (mode == 2 && !workspace))
+    return AST_E_NULLPTR;
+  if (act != 0 && act != 1) return AST_E_UNSUPPORTED;
   if (mode < 0 || mode > 2) return AST_E_UNSUPPORTED;
   if (n <= 0 || c <= 0 || h <= 0 || wd <= 0 || (k != 3 && k != 5) || (s != 1 && s != 2)) return AST_E_SHAPE;
   const int p = (k - 1) / 2;
@@ -397,7 +411,7 @@ int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, flo
   const int ho = (h + 2 * p - k) / s + 1, wo = (wd + 2 * p - k) / s + 1;
   const int64_t nc = (int64_t)n * c;
   if (nc * (h + 2 * p) * (wd + 2 * p) >= (1LL << 31) || n > 65535 || c > 65535) return AST_E_SHAPE;  // 32-bit indices
-  DwArgs a{x, w, g, out, workspace, n, c, h, wd, ho, wo, 0, {}, (hipStream_t)stream};
+  DwArgs a{x, w, g, out, workspace, n, c, h, wd, ho, wo, 0, act, {}, (hipStream_t)stream};
   if (mode == 0) {
     a.p = dw_plan(ho, wo);
     dw_launch<FwdL>(k, s, a.p, a);
@@ -415,6 +429,11 @@ int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, flo
     if (e != hipSuccess) return (int)e;
   }
   return (int)hipGetLastError();
+}
+
+int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, float* out, int n, int c, int h, int wd,
+                   int k, int s, float* workspace, long long workspace_floats, void* stream) {
+  return ast_mbt_dw_act_f32(mode, x, w, g, out, n, c, h, wd, k, s, 0, workspace, workspace_floats, stream);
 }
 
 }  // extern "C"

@@ -560,7 +560,22 @@ __global__ void bn_merge_stats_kernel(const double* __restrict__ stats, int part
   if (inv_count && ch == 0) inv_count[0] = (float)(1.0 / na);
 }
 
-// grid (chunks of 4*kT pixels, planes (strided by gridDim.y))
+// op 0 hardswish(a), 1 hardswish backward (x = a, g = b; torch: x < -3: 0; x <= 3: g (x/3 + 1/2);
+// else g), 2 a + b
+template <int OP>
+__device__ __forceinline__ float elt(float a, float b) {
+  if (OP == 0) return a * fminf(fmaxf(a + 3.f, 0.f), 6.f) / 6.f;
+  if (OP == 1) return a < -3.f ? 0.f : (a <= 3.f ? b * (a / 3.f + 0.5f) : b);
+  return a + b;
+}
+
+// the BatchNorm affine, one expression for the forward and the backward's recomputation (so a
+// fused Hardswish sees bit-identical inputs in both)
+__device__ __forceinline__ float bn_aff(float x, float mu, float sc, float bt) { return (x - mu) * sc + bt; }
+
+// grid (chunks of 4*kT pixels, planes (strided by gridDim.y)); ACT 1: Hardswish of the output
+// (DepthWiseConv's BatchNorm2d -> Hardswish pair, mobilenetv2.py:122-126, in one pass)
+template <int ACT>
 __global__ __launch_bounds__(kT) void bn_apply_kernel(const float* __restrict__ x, int c, int64_t hw, int planes,
                                                       const float* __restrict__ mean, const float* __restrict__ invstd,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -573,25 +588,34 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const float* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t i = (int64_t)blockIdx.x * 4 * kT + j * kT + threadIdx.x;
-      if (i < hw) yp[i] = (xp[i] - mu) * sc + bt;
+      if (i < hw) {
+        const float v = bn_aff(xp[i], mu, sc, bt);
+        yp[i] = ACT ? elt<0>(v, 0.f) : v;
+      }
     }
   }
 }
 
-// per (segment, image, channel): sum(dy), sum(dy * xhat)
+// per (segment, image, channel): sum(dy), sum(dy * xhat); ACT 1: dy is the gradient of
+// Hardswish(BN(x)), taken through the Hardswish at the recomputed BN output
+template <int ACT>
 __global__ __launch_bounds__(kT) void bn_part_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                          int c, int64_t hw, const float* __restrict__ mean,
-                                                         const float* __restrict__ invstd, float* __restrict__ part) {
+                                                         const float* __restrict__ invstd,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* __restrict__ part) {
   __shared__ float sh[kT / 64];
   const int sx = blockIdx.x, b = blockIdx.y, ch = blockIdx.z;
   const int64_t o = ((int64_t)b * c + ch) * hw + (int64_t)sx * BN_SEG;
   const int len = (int)min((int64_t)BN_SEG, hw - (int64_t)sx * BN_SEG);
   const float mu = mean[ch], is = invstd[ch];
+  const float sc = ACT ? is * (gamma ? gamma[ch] : 1.f) : 0.f, bt = ACT && beta ? beta[ch] : 0.f;
   float s1 = 0.f, s2 = 0.f;
   for (int i = threadIdx.x; i < len; i += kT) {
-    const float gv = dy[o + i];
+    const float xv = x[o + i];
+    const float gv = ACT ? elt<1>(bn_aff(xv, mu, sc, bt), dy[o + i]) : dy[o + i];
     s1 += gv;
-    s2 = fmaf(gv, (x[o + i] - mu) * is, s2);
+    s2 = fmaf(gv, (xv - mu) * is, s2);
   }
   s1 = block_sum(s1, sh);
   s2 = block_sum(s2, sh);
@@ -618,25 +642,30 @@ __global__ void bn_finalize_bwd_kernel(const float* __restrict__ part, int S, in
   if (inv_count && ch == 0) inv_count[0] = inv_value;
 }
 
+template <int ACT>
 __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                           int c, int64_t hw, int planes,
                                                           const float* __restrict__ inv_count,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
                                                           const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta,
                                                           const float* __restrict__ sdy,
                                                           const float* __restrict__ sdyx, float* __restrict__ dx) {
   for (int pl = blockIdx.y; pl < planes; pl += gridDim.y) {
     const int ch = pl % c;
     const float is = invstd[ch], mu = mean[ch], gm = (gamma ? gamma[ch] : 1.f) * is;
+    const float bt = ACT && beta ? beta[ch] : 0.f;
     const float inv_m = inv_count[0], a = sdy[ch] * inv_m, bq = sdyx[ch] * inv_m;
     const int64_t base = (int64_t)pl * hw;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t i = (int64_t)blockIdx.x * 4 * kT + j * kT + threadIdx.x;
       if (i < hw) {
-        const float xh = (x[base + i] - mu) * is;
-        dx[base + i] = gm * (dy[base + i] - a - xh * bq);
+        const float xv = x[base + i];
+        const float gv = ACT ? elt<1>(bn_aff(xv, mu, gm, bt), dy[base + i]) : dy[base + i];
+        const float xh = (xv - mu) * is;
+        dx[base + i] = gm * (gv - a - xh * bq);
       }
     }
   }
@@ -645,17 +674,10 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restric
 // ------------------------------------------------------------------------------------------------
 // elementwise
 // ------------------------------------------------------------------------------------------------
-// op 0 hardswish(a), 1 hardswish backward (x = a, g = b; torch: x < -3: 0; x <= 3: g (x/3 + 1/2);
-// else g), 2 a + b. Four elements per thread, as one 16-byte access when the host saw n % 4 == 0
-// and 16-byte aligned pointers.
+// eltwise_kernel: elt<OP> over four elements per thread, as one 16-byte access when the host saw
+// n % 4 == 0 and 16-byte aligned pointers.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int OP>
-__device__ __forceinline__ float elt(float a, float b) {
-  if (OP == 0) return a * fminf(fmaxf(a + 3.f, 0.f), 6.f) / 6.f;
-  if (OP == 1) return a < -3.f ? 0.f : (a <= 3.f ? b * (a / 3.f + 0.5f) : b);
-  return a + b;
-}
 
 template <int OP, bool V4>
 __global__ __launch_bounds__(kT) void eltwise_kernel(const float* __restrict__ a, const float* __restrict__ b,
@@ -701,7 +723,11 @@ __global__ void up2_bwd_kernel(const float* __restrict__ g, float* __restrict__ 
   }
 }
 
-// per-plane mean (SE AdaptiveAvgPool2d(1)) or, with y, per-plane sum(x * y) (the gate gradient)
+// per-plane mean (SE AdaptiveAvgPool2d(1)) or, with y, per-plane sum(x * y) (the gate gradient).
+// ACT 1: the SE input is hardswish of the stored tensor (DepthWiseConv's Hardswish -> SELayer,
+// mobilenetv2.py:151-156, without materialising the activation): mean(hardswish(x)), or
+// sum(x * hardswish(y)).
+template <int ACT>
 __global__ __launch_bounds__(kT) void plane_dot_kernel(const float* __restrict__ x, const float* __restrict__ y,
                                                        int64_t hw, float scale, float* __restrict__ out) {
   __shared__ float sh[kT / 64];
@@ -709,24 +735,35 @@ __global__ __launch_bounds__(kT) void plane_dot_kernel(const float* __restrict__
   const float* xp = x + p * hw;
   const float* yp = y ? y + p * hw : nullptr;
   float s = 0.f;
-  for (int64_t i = threadIdx.x; i < hw; i += kT) s += yp ? xp[i] * yp[i] : xp[i];
+  for (int64_t i = threadIdx.x; i < hw; i += kT) {
+    if (yp) s += xp[i] * (ACT ? elt<0>(yp[i], 0.f) : yp[i]);
+    else s += ACT ? elt<0>(xp[i], 0.f) : xp[i];
+  }
   const float t = block_sum(s, sh);
   if (threadIdx.x == 0) out[p] = t * scale;
 }
 
-// y = x * gate[plane] (+ gadd[plane] when given: the SE input gradient dy*g + dpool/hw);
-// grid (chunks of 4*kT pixels, planes strided by gridDim.y)
+// OP 0: y = x * gate[plane] (+ gadd[plane] when given: the SE input gradient dy*g + dpool/hw);
+// OP 1: y = hardswish(x) * gate[plane] (the SE output over the un-materialised activation);
+// OP 2: y = hardswish'(a) * (x * gate[plane] + gadd[plane]) (the SE input gradient taken on
+// through the Hardswish at its input a). grid (chunks of 4*kT pixels, planes strided by gridDim.y)
+template <int OP>
 __global__ __launch_bounds__(kT) void plane_scale_kernel(const float* __restrict__ x, const float* __restrict__ gate,
-                                                         const float* __restrict__ gadd, int64_t hw, int64_t planes,
-                                                         float* __restrict__ y) {
+                                                         const float* __restrict__ gadd, const float* __restrict__ a,
+                                                         int64_t hw, int64_t planes, float* __restrict__ y) {
   for (int64_t p = blockIdx.y; p < planes; p += gridDim.y) {
     const float gv = gate[p], av = gadd ? gadd[p] : 0.f;
     const float* xp = x + p * hw;
+    const float* ap = OP == 2 ? a + p * hw : nullptr;
     float* yp = y + p * hw;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t i = (int64_t)blockIdx.x * 4 * kT + j * kT + threadIdx.x;
-      if (i < hw) yp[i] = fmaf(xp[i], gv, av);
+      if (i < hw) {
+        if (OP == 0) yp[i] = fmaf(xp[i], gv, av);
+        else if (OP == 1) yp[i] = elt<0>(xp[i], 0.f) * gv;
+        else yp[i] = elt<1>(ap[i], fmaf(xp[i], gv, av));
+      }
     }
   }
 }
@@ -940,69 +977,129 @@ int ast_mbt_bn_merge_f32(const double* stats, int parts, int c, float eps, float
   return (int)hipGetLastError();
 }
 
-int ast_mbt_bn_apply_f32(const float* x, int n, int c, long long hw, const float* mean, const float* invstd,
-                         const float* gamma, const float* beta, float* y, void* stream) {
+int ast_mbt_bn_act_apply_f32(const float* x, int n, int c, long long hw, const float* mean, const float* invstd,
+                             const float* gamma, const float* beta, int act, float* y, void* stream) {
   if (!x || !mean || !invstd || !y) return AST_E_NULLPTR;
   if (n <= 0 || c <= 0 || hw <= 0 || (int64_t)n * c > 0x7fffffffLL) return AST_E_SHAPE;
-  hipLaunchKernelGGL(bn_apply_kernel, plane_grid(hw, (int64_t)n * c), dim3(kT), 0, (hipStream_t)stream, x, c,
-                     (int64_t)hw, n * c, mean, invstd, gamma, beta, y);
+  if (act != 0 && act != 1) return AST_E_UNSUPPORTED;
+  const dim3 grid = plane_grid(hw, (int64_t)n * c);
+  if (act)
+    hipLaunchKernelGGL(bn_apply_kernel<1>, grid, dim3(kT), 0, (hipStream_t)stream, x, c, (int64_t)hw, n * c, mean,
+                       invstd, gamma, beta, y);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<0>, grid, dim3(kT), 0, (hipStream_t)stream, x, c, (int64_t)hw, n * c, mean,
+                       invstd, gamma, beta, y);
   return (int)hipGetLastError();
 }
 
-int ast_mbt_bn_fwd_f32(const float* x, int n, int c, long long hw, const float* gamma, const float* beta, float eps,
-                       float momentum, float* mean, float* invstd, float* run_mean, float* run_var, float* y,
-                       float* workspace, long long workspace_floats, void* stream) {
+int ast_mbt_bn_apply_f32(const float* x, int n, int c, long long hw, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, float* y, void* stream) {
+  return ast_mbt_bn_act_apply_f32(x, n, c, hw, mean, invstd, gamma, beta, 0, y, stream);
+}
+
+int ast_mbt_bn_act_fwd_f32(const float* x, int n, int c, long long hw, const float* gamma, const float* beta,
+                           float eps, float momentum, float* mean, float* invstd, float* run_mean, float* run_var,
+                           int act, float* y, float* workspace, long long workspace_floats, void* stream) {
   if (!x || !mean || !invstd || !y) return AST_E_NULLPTR;
   if (int e = bn_check(n, c, hw, workspace, workspace_floats)) return e;
   const long long off = ast_mbt_bn_workspace_floats(n, c, hw) - 6LL * c - 2;
   double* stats = (double*)(workspace + off);
   int e = ast_mbt_bn_stats_f32(x, n, c, hw, workspace, workspace_floats, stats, stream);
   if (!e) e = ast_mbt_bn_merge_f32(stats, 1, c, eps, momentum, mean, invstd, run_mean, run_var, nullptr, stream);
-  if (!e) e = ast_mbt_bn_apply_f32(x, n, c, hw, mean, invstd, gamma, beta, y, stream);
+  if (!e) e = ast_mbt_bn_act_apply_f32(x, n, c, hw, mean, invstd, gamma, beta, act, y, stream);
   return e;
+}
+
+int ast_mbt_bn_fwd_f32(const float* x, int n, int c, long long hw, const float* gamma, const float* beta, float eps,
+                       float momentum, float* mean, float* invstd, float* run_mean, float* run_var, float* y,
+                       float* workspace, long long workspace_floats, void* stream) {
+  return ast_mbt_bn_act_fwd_f32(x, n, c, hw, gamma, beta, eps, momentum, mean, invstd, run_mean, run_var, 0, y,
+                                workspace, workspace_floats, stream);
+}
+
+static void bn_part_bwd(int act, int segs, int n, int c, const float* x, const float* dy, long long hw,
+                        const float* mean, const float* invstd, const float* gamma, const float* beta, float* part,
+                        hipStream_t st) {
+  if (act)
+    hipLaunchKernelGGL(bn_part_bwd_kernel<1>, dim3(segs, n, c), dim3(kT), 0, st, x, dy, c, (int64_t)hw, mean, invstd,
+                       gamma, beta, part);
+  else
+    hipLaunchKernelGGL(bn_part_bwd_kernel<0>, dim3(segs, n, c), dim3(kT), 0, st, x, dy, c, (int64_t)hw, mean, invstd,
+                       gamma, beta, part);
+}
+
+static void bn_bwd_apply(int act, int n, int c, const float* x, const float* dy, long long hw,
+                         const float* inv_count, const float* mean, const float* invstd, const float* gamma,
+                         const float* beta, const float* sdy, const float* sdyx, float* dx, hipStream_t st) {
+  const dim3 grid = plane_grid(hw, (int64_t)n * c);
+  if (act)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(kT), 0, st, x, dy, c, (int64_t)hw, n * c, inv_count, mean,
+                       invstd, gamma, beta, sdy, sdyx, dx);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<0>, grid, dim3(kT), 0, st, x, dy, c, (int64_t)hw, n * c, inv_count, mean,
+                       invstd, gamma, beta, sdy, sdyx, dx);
+}
+
+int ast_mbt_bn_act_bwd_sums_f32(const float* x, const float* dy, int n, int c, long long hw, const float* mean,
+                                const float* invstd, const float* gamma, const float* beta, int act,
+                                float* workspace, long long workspace_floats, float* sums, void* stream) {
+  if (!x || !dy || !mean || !invstd || !sums) return AST_E_NULLPTR;
+  if (act != 0 && act != 1) return AST_E_UNSUPPORTED;
+  if (int e = bn_check(n, c, hw, workspace, workspace_floats)) return e;
+  hipStream_t st = (hipStream_t)stream;
+  const int segs = (int)((hw + BN_SEG - 1) / BN_SEG);
+  bn_part_bwd(act, segs, n, c, x, dy, hw, mean, invstd, gamma, beta, workspace, st);
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((c + 63) / 64), dim3(64), 0, st, workspace, segs * n, c, sums,
+                     sums + c, nullptr, 0.f);
+  return (int)hipGetLastError();
 }
 
 int ast_mbt_bn_bwd_sums_f32(const float* x, const float* dy, int n, int c, long long hw, const float* mean,
                             const float* invstd, float* workspace, long long workspace_floats, float* sums,
                             void* stream) {
-  if (!x || !dy || !mean || !invstd || !sums) return AST_E_NULLPTR;
-  if (int e = bn_check(n, c, hw, workspace, workspace_floats)) return e;
-  hipStream_t st = (hipStream_t)stream;
-  const int segs = (int)((hw + BN_SEG - 1) / BN_SEG);
-  hipLaunchKernelGGL(bn_part_bwd_kernel, dim3(segs, n, c), dim3(kT), 0, st, x, dy, c, (int64_t)hw, mean, invstd,
-                     workspace);
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((c + 63) / 64), dim3(64), 0, st, workspace, segs * n, c, sums,
-                     sums + c, nullptr, 0.f);
+  return ast_mbt_bn_act_bwd_sums_f32(x, dy, n, c, hw, mean, invstd, nullptr, nullptr, 0, workspace,
+                                     workspace_floats, sums, stream);
+}
+
+int ast_mbt_bn_act_bwd_apply_f32(const float* x, const float* dy, int n, int c, long long hw, const float* mean,
+                                 const float* invstd, const float* gamma, const float* beta, int act,
+                                 const float* sums, const float* inv_count, float* dx, void* stream) {
+  if (!x || !dy || !mean || !invstd || !sums || !inv_count || !dx) return AST_E_NULLPTR;
+  if (n <= 0 || c <= 0 || hw <= 0 || (int64_t)n * c > 0x7fffffffLL) return AST_E_SHAPE;
+  if (act != 0 && act != 1) return AST_E_UNSUPPORTED;
+  bn_bwd_apply(act, n, c, x, dy, hw, inv_count, mean, invstd, gamma, beta, sums, sums + c, dx, (hipStream_t)stream);
   return (int)hipGetLastError();
 }
 
 int ast_mbt_bn_bwd_apply_f32(const float* x, const float* dy, int n, int c, long long hw, const float* mean,
                              const float* invstd, const float* gamma, const float* sums, const float* inv_count,
                              float* dx, void* stream) {
-  if (!x || !dy || !mean || !invstd || !sums || !inv_count || !dx) return AST_E_NULLPTR;
-  if (n <= 0 || c <= 0 || hw <= 0 || (int64_t)n * c > 0x7fffffffLL) return AST_E_SHAPE;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, plane_grid(hw, (int64_t)n * c), dim3(kT), 0, (hipStream_t)stream, x, dy, c,
-                     (int64_t)hw, n * c, inv_count, mean, invstd, gamma, sums, sums + c, dx);
-  return (int)hipGetLastError();
+  return ast_mbt_bn_act_bwd_apply_f32(x, dy, n, c, hw, mean, invstd, gamma, nullptr, 0, sums, inv_count, dx, stream);
 }
 
-int ast_mbt_bn_bwd_f32(const float* x, const float* dy, int n, int c, long long hw, const float* mean,
-                       const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dx,
-                       float* workspace, long long workspace_floats, void* stream) {
+int ast_mbt_bn_act_bwd_f32(const float* x, const float* dy, int n, int c, long long hw, const float* mean,
+                           const float* invstd, const float* gamma, const float* beta, int act, float* dgamma,
+                           float* dbeta, float* dx, float* workspace, long long workspace_floats, void* stream) {
   if (!dgamma || !dbeta) return AST_E_NULLPTR;
+  if (act != 0 && act != 1) return AST_E_UNSUPPORTED;
   if (int e = bn_check(n, c, hw, workspace, workspace_floats)) return e;
   if (!x || !dy || !mean || !invstd || !dx) return AST_E_NULLPTR;
   const long long off = ast_mbt_bn_workspace_floats(n, c, hw) - 6LL * c - 2;
   float* inv_count = workspace + off;
   hipStream_t st = (hipStream_t)stream;
   const int segs = (int)((hw + BN_SEG - 1) / BN_SEG);
-  hipLaunchKernelGGL(bn_part_bwd_kernel, dim3(segs, n, c), dim3(kT), 0, st, x, dy, c, (int64_t)hw, mean, invstd,
-                     workspace);
+  bn_part_bwd(act, segs, n, c, x, dy, hw, mean, invstd, gamma, beta, workspace, st);
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((c + 63) / 64), dim3(64), 0, st, workspace, segs * n, c, dbeta,
                      dgamma, inv_count, (float)(1.0 / ((double)n * (double)hw)));
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, plane_grid(hw, (int64_t)n * c), dim3(kT), 0, st, x, dy, c, (int64_t)hw,
-                     n * c, inv_count, mean, invstd, gamma, dbeta, dgamma, dx);
+  bn_bwd_apply(act, n, c, x, dy, hw, inv_count, mean, invstd, gamma, beta, dbeta, dgamma, dx, st);
   return (int)hipGetLastError();
+}
+
+int ast_mbt_bn_bwd_f32(const float* x, const float* dy, int n, int c, long long hw, const float* mean,
+                       const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dx,
+                       float* workspace, long long workspace_floats, void* stream) {
+  return ast_mbt_bn_act_bwd_f32(x, dy, n, c, hw, mean, invstd, gamma, nullptr, 0, dgamma, dbeta, dx, workspace,
+                                workspace_floats, stream);
 }
 
 int ast_mbt_eltwise_f32(int op, const float* a, const float* b, float* y, long long n, int h, int w, void* stream) {
@@ -1033,21 +1130,49 @@ int ast_mbt_eltwise_f32(int op, const float* a, const float* b, float* y, long l
   return (int)hipGetLastError();
 }
 
-int ast_mbt_plane_f32(int op, const float* x, const float* y, const float* gate, const float* gadd, float* out,
-                      long long planes, long long hw, void* stream) {
-  // op 0: out[p] = mean(x[p]); 1: out[p] = sum(x[p] * y[p]); 2: out = x * gate[p] (+ gadd[p])
-  if (!x || !out || (op == 1 && !y) || (op == 2 && !gate)) return AST_E_NULLPTR;
+int ast_mbt_plane_act_f32(int op, const float* x, const float* y, const float* gate, const float* gadd,
+                          const float* a, float* out, long long planes, long long hw, void* stream) {
+  // op 0: out[p] = mean(x[p]); 1: out[p] = sum(x[p] * y[p]); 2: out = x * gate[p] (+ gadd[p]);
+  //    3: out[p] = mean(hardswish(x[p])); 4: out[p] = sum(x[p] * hardswish(y[p]));
+  //    5: out = hardswish(x) * gate[p]; 6: out = hardswish'(a) * (x * gate[p] + gadd[p])
+  if (!x || !out || ((op == 1 || op == 4) && !y) || ((op == 2 || op == 5 || op == 6) && !gate) || (op == 6 && !a))
+    return AST_E_NULLPTR;
   if (planes <= 0 || hw <= 0 || planes > 0x7fffffffLL) return AST_E_SHAPE;
   hipStream_t st = (hipStream_t)stream;
-  if (op == 0 || op == 1)
-    hipLaunchKernelGGL(plane_dot_kernel, dim3((unsigned)planes), dim3(kT), 0, st, x, op == 1 ? y : nullptr,
-                       (int64_t)hw, op == 0 ? 1.0f / (float)hw : 1.0f, out);
-  else if (op == 2)
-    hipLaunchKernelGGL(plane_scale_kernel, plane_grid(hw, planes), dim3(kT), 0, st, x, gate, gadd, (int64_t)hw,
-                       (int64_t)planes, out);
-  else
-    return AST_E_UNSUPPORTED;
+  const dim3 pg((unsigned)planes);
+  switch (op) {
+    case 0:
+    case 1:
+      hipLaunchKernelGGL(plane_dot_kernel<0>, pg, dim3(kT), 0, st, x, op == 1 ? y : nullptr, (int64_t)hw,
+                         op == 0 ? 1.0f / (float)hw : 1.0f, out);
+      break;
+    case 3:
+    case 4:
+      hipLaunchKernelGGL(plane_dot_kernel<1>, pg, dim3(kT), 0, st, x, op == 4 ? y : nullptr, (int64_t)hw,
+                         op == 3 ? 1.0f / (float)hw : 1.0f, out);
+      break;
+    case 2:
+      hipLaunchKernelGGL(plane_scale_kernel<0>, plane_grid(hw, planes), dim3(kT), 0, st, x, gate, gadd, nullptr,
+                         (int64_t)hw, (int64_t)planes, out);
+      break;
+    case 5:
+      hipLaunchKernelGGL(plane_scale_kernel<1>, plane_grid(hw, planes), dim3(kT), 0, st, x, gate, nullptr, nullptr,
+                         (int64_t)hw, (int64_t)planes, out);
+      break;
+    case 6:
+      hipLaunchKernelGGL(plane_scale_kernel<2>, plane_grid(hw, planes), dim3(kT), 0, st, x, gate, gadd, a,
+                         (int64_t)hw, (int64_t)planes, out);
+      break;
+    default:
+      return AST_E_UNSUPPORTED;
+  }
   return (int)hipGetLastError();
+}
+
+int ast_mbt_plane_f32(int op, const float* x, const float* y, const float* gate, const float* gadd, float* out,
+                      long long planes, long long hw, void* stream) {
+  if (op < 0 || op > 2) return AST_E_UNSUPPORTED;
+  return ast_mbt_plane_act_f32(op, x, y, gate, gadd, nullptr, out, planes, hw, stream);
 }
 
 int ast_mbt_se_fc_fwd_f32(const float* pool, const float* w1, const float* b1, const float* w2, const float* b2,

@@ -10,6 +10,8 @@ nearest upsample. fp32 only (the reference trains in fp32).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -103,19 +105,22 @@ class PwConvFn(torch.autograd.Function):
 
 
 class DwConvFn(torch.autograd.Function):
-    """Depthwise k x k conv, stride s, reflect padding (k-1)/2."""
+    """Depthwise k x k conv, stride s, reflect padding (k-1)/2. act = 1: the conv's input is
+    hardswish(x), x the pre-activation (the block's Hardswish fused into the staging; the backward
+    returns the gradient w.r.t. x)."""
 
     @staticmethod
-    def forward(ctx, x, weight, k, s):
+    def forward(ctx, x, weight, k, s, act=0):
         x = _f32(x, "x")
         n, c, h, w = x.shape
         p = (k - 1) // 2
         ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
         wt = weight.detach().reshape(c, k * k).contiguous()
         y = torch.empty((n, c, ho, wo), device=x.device, dtype=torch.float32)
-        check(lib().ast_mbt_dw_f32(0, ptr(x), ptr(wt), None, ptr(y), n, c, h, w, k, s, None, 0, _s(x)), "dw conv")
+        check(lib().ast_mbt_dw_act_f32(0, ptr(x), ptr(wt), None, ptr(y), n, c, h, w, k, s, int(act), None, 0, _s(x)),
+              "dw conv")
         ctx.save_for_backward(x, wt)
-        ctx.k, ctx.s, ctx.wshape = k, s, weight.shape
+        ctx.k, ctx.s, ctx.act, ctx.wshape = k, s, int(act), weight.shape
         return y
 
     @staticmethod
@@ -126,15 +131,15 @@ class DwConvFn(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            check(lib().ast_mbt_dw_f32(1, None, ptr(wt), ptr(g), ptr(dx), n, c, h, w, ctx.k, ctx.s, None, 0, _s(g)),
-                  "dw dgrad")
+            check(lib().ast_mbt_dw_act_f32(1, ptr(x) if ctx.act else None, ptr(wt), ptr(g), ptr(dx), n, c, h, w, ctx.k,
+                                           ctx.s, ctx.act, None, 0, _s(g)), "dw dgrad")
         if ctx.needs_input_grad[1]:
             dw = torch.empty((c, ctx.k * ctx.k), device=g.device, dtype=torch.float32)
             ws = workspace(lib().ast_mbt_dw_workspace_floats(n, c, h, w, ctx.k), x.device)
-            check(lib().ast_mbt_dw_f32(2, ptr(x), ptr(wt), ptr(g), ptr(dw), n, c, h, w, ctx.k, ctx.s, ptr(ws), ws.numel(),
-                                       _s(g)), "dw wgrad")
+            check(lib().ast_mbt_dw_act_f32(2, ptr(x), ptr(wt), ptr(g), ptr(dw), n, c, h, w, ctx.k, ctx.s, ctx.act,
+                                           ptr(ws), ws.numel(), _s(g)), "dw wgrad")
             dw = dw.reshape(ctx.wshape)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 def _bn_workspace(x, n, c, hw):
@@ -142,12 +147,15 @@ def _bn_workspace(x, n, c, hw):
 
 
 class BatchNormTrainFn(torch.autograd.Function):
-    """BatchNorm2d.forward in training mode (batch statistics; running stats updated in place).
-    A BatchNorm marked by dp.convert_sync_batchnorm takes its statistics over every rank's images
-    (all-gather of per-rank (count, mean, M2), all-reduce of the backward sums)."""
+    """BatchNorm2d.forward in training mode (batch statistics; running stats updated in place),
+    with `act` = 1 the following Hardswish fused in (DepthWiseConv's BN -> Hardswish pairs,
+    mobilenetv2.py:122-126, :150-153): one apply pass writes hardswish(BN(x)), and the backward
+    takes the Hardswish derivative at the recomputed BN output inside its two passes (the BN output
+    is never stored). A BatchNorm marked by dp.convert_sync_batchnorm takes its statistics over
+    every rank's images (all-gather of per-rank (count, mean, M2), all-reduce of the backward sums)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, bn):
+    def forward(ctx, x, gamma, beta, bn, act=0):
         x = _f32(x, "x")
         n, c, h, w = x.shape
         mean = torch.empty((c,), device=x.device, dtype=torch.float32)
@@ -159,12 +167,12 @@ class BatchNormTrainFn(torch.autograd.Function):
         rm = ptr(bn.running_mean) if track else None
         rv = ptr(bn.running_var) if track else None
         group = dp.sync_group(bn)
-        ctx.group = group
+        ctx.group, ctx.act = group, int(act)
         inv_count = None
         if group is None:
-            check(lib().ast_mbt_bn_fwd_f32(ptr(x), n, c, h * w, ptr(gamma), ptr(beta), float(bn.eps), float(momentum),
-                                           ptr(mean), ptr(invstd), rm, rv, ptr(y), ptr(ws), ws.numel(), _s(x)),
-                  "batch norm")
+            check(lib().ast_mbt_bn_act_fwd_f32(ptr(x), n, c, h * w, ptr(gamma), ptr(beta), float(bn.eps),
+                                               float(momentum), ptr(mean), ptr(invstd), rm, rv, ctx.act, ptr(y),
+                                               ptr(ws), ws.numel(), _s(x)), "batch norm")
         else:
             L = lib()
             stats = torch.empty((c, 3), device=x.device, dtype=torch.float64)
@@ -173,16 +181,16 @@ class BatchNormTrainFn(torch.autograd.Function):
             inv_count = torch.empty((1,), device=x.device, dtype=torch.float32)
             check(L.ast_mbt_bn_merge_f32(ptr(allst), allst.shape[0], c, float(bn.eps), float(momentum), ptr(mean),
                                          ptr(invstd), rm, rv, ptr(inv_count), _s(x)), "bn merge")
-            check(L.ast_mbt_bn_apply_f32(ptr(x), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta), ptr(y),
-                                         _s(x)), "bn apply")
+            check(L.ast_mbt_bn_act_apply_f32(ptr(x), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
+                                             ctx.act, ptr(y), _s(x)), "bn apply")
         if track:
             bn.num_batches_tracked.add_(1)   # bookkeeping counter (torch does the same host-side increment)
-        ctx.save_for_backward(x, gamma, mean, invstd, inv_count if inv_count is not None else mean)
+        ctx.save_for_backward(x, gamma, beta, mean, invstd, inv_count if inv_count is not None else mean)
         return y
 
     @staticmethod
     def backward(ctx, g):
-        x, gamma, mean, invstd, inv_count = ctx.saved_tensors
+        x, gamma, beta, mean, invstd, inv_count = ctx.saved_tensors
         g = _f32(g, "grad")
         n, c, h, w = x.shape
         dx = torch.empty_like(x)
@@ -190,19 +198,21 @@ class BatchNormTrainFn(torch.autograd.Function):
         if ctx.group is None:
             dgamma = torch.empty_like(mean)
             dbeta = torch.empty_like(mean)
-            check(lib().ast_mbt_bn_bwd_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma),
-                                           ptr(dgamma), ptr(dbeta), ptr(dx), ptr(ws), ws.numel(), _s(g)),
-                  "batch norm backward")
-            return dx, dgamma, dbeta, None
+            check(lib().ast_mbt_bn_act_bwd_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma),
+                                               ptr(beta), ctx.act, ptr(dgamma), ptr(dbeta), ptr(dx), ptr(ws),
+                                               ws.numel(), _s(g)), "batch norm backward")
+            return dx, dgamma, dbeta, None, None
         L = lib()
         sums = torch.empty((2, c), device=x.device, dtype=torch.float32)
-        check(L.ast_mbt_bn_bwd_sums_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(ws), ws.numel(),
-                                        ptr(sums), _s(g)), "bn backward sums")
+        check(L.ast_mbt_bn_act_bwd_sums_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma),
+                                            ptr(beta), ctx.act, ptr(ws), ws.numel(), ptr(sums), _s(g)),
+              "bn backward sums")
         dbeta, dgamma = sums[0].clone(), sums[1].clone()     # local: the gradient all-reduce averages them
         dp.all_reduce_sum(sums, ctx.group)
-        check(L.ast_mbt_bn_bwd_apply_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma), ptr(sums),
-                                         ptr(inv_count), ptr(dx), _s(g)), "bn backward apply")
-        return dx, dgamma, dbeta, None
+        check(L.ast_mbt_bn_act_bwd_apply_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma),
+                                             ptr(beta), ctx.act, ptr(sums), ptr(inv_count), ptr(dx), _s(g)),
+              "bn backward apply")
+        return dx, dgamma, dbeta, None, None
 
 
 class HardswishFn(torch.autograd.Function):
@@ -259,24 +269,31 @@ class Upsample2Fn(torch.autograd.Function):
 
 
 class SEFn(torch.autograd.Function):
-    """SELayer.forward (mobilenetv2.py:72-81): x * Hardtanh(0,1)(fc2(relu(fc1(avgpool(x)))))."""
+    """SELayer.forward (mobilenetv2.py:72-81): x * Hardtanh(0,1)(fc2(relu(fc1(avgpool(x))))).
+    act = 1: the SE input is hardswish(x), x the pre-activation (the block's Hardswish fused into
+    the pool and scale passes; the backward returns the gradient w.r.t. x)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
+    def forward(ctx, x, w1, b1, w2, b2, act=0):
         x = _f32(x, "x")
         n, c, h, w = x.shape
         red = w1.shape[0]
+        act = int(act)
         pool = torch.empty((n, c), device=x.device, dtype=torch.float32)
-        check(lib().ast_mbt_plane_f32(0, ptr(x), None, None, None, ptr(pool), n * c, h * w, _s(x)), "se pool")
+        L = lib()
+        check(L.ast_mbt_plane_act_f32(3 if act else 0, ptr(x), None, None, None, None, ptr(pool), n * c, h * w, _s(x)),
+              "se pool")
         hid = torch.empty((n, red), device=x.device, dtype=torch.float32)
         z = torch.empty((n, c), device=x.device, dtype=torch.float32)
         gate = torch.empty_like(z)
         w1c, w2c = w1.detach().contiguous(), w2.detach().contiguous()
-        check(lib().ast_mbt_se_fc_fwd_f32(ptr(pool), ptr(w1c), ptr(b1), ptr(w2c), ptr(b2), n, c, red, ptr(hid), ptr(z),
-                                          ptr(gate), _s(x)), "se fc")
+        check(L.ast_mbt_se_fc_fwd_f32(ptr(pool), ptr(w1c), ptr(b1), ptr(w2c), ptr(b2), n, c, red, ptr(hid), ptr(z),
+                                      ptr(gate), _s(x)), "se fc")
         y = torch.empty_like(x)
-        check(lib().ast_mbt_plane_f32(2, ptr(x), None, ptr(gate), None, ptr(y), n * c, h * w, _s(x)), "se scale")
+        check(L.ast_mbt_plane_act_f32(5 if act else 2, ptr(x), None, ptr(gate), None, None, ptr(y), n * c, h * w,
+                                      _s(x)), "se scale")
         ctx.save_for_backward(x, w1c, w2c, pool, hid, z, gate)
+        ctx.act = act
         return y
 
     @staticmethod
@@ -285,19 +302,26 @@ class SEFn(torch.autograd.Function):
         g = _f32(g, "grad")
         n, c, h, w = x.shape
         red = w1.shape[0]
+        L = lib()
         dgate = torch.empty((n, c), device=x.device, dtype=torch.float32)
-        check(lib().ast_mbt_plane_f32(1, ptr(g), ptr(x), None, None, ptr(dgate), n * c, h * w, _s(g)), "se dgate")
+        check(L.ast_mbt_plane_act_f32(4 if ctx.act else 1, ptr(g), ptr(x), None, None, None, ptr(dgate), n * c, h * w,
+                                      _s(g)), "se dgate")
         dw1, db1 = torch.empty_like(w1), torch.empty((red,), device=x.device, dtype=torch.float32)
         dw2, db2 = torch.empty_like(w2), torch.empty((c,), device=x.device, dtype=torch.float32)
         dpool = torch.empty((n, c), device=x.device, dtype=torch.float32)
         ws = workspace(n * (c + red), x.device)
-        check(lib().ast_mbt_se_fc_bwd_f32(ptr(dgate), ptr(z), ptr(hid), ptr(pool), ptr(w1), ptr(w2), n, c, red, h * w,
-                                          ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), ptr(dpool), ptr(ws), ws.numel(),
-                                          _s(g)), "se fc bwd")
+        check(L.ast_mbt_se_fc_bwd_f32(ptr(dgate), ptr(z), ptr(hid), ptr(pool), ptr(w1), ptr(w2), n, c, red, h * w,
+                                      ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), ptr(dpool), ptr(ws), ws.numel(), _s(g)),
+              "se fc bwd")
         dx = torch.empty_like(x)
-        check(lib().ast_mbt_plane_f32(2, ptr(g), None, ptr(gate), ptr(dpool), ptr(dx), n * c, h * w, _s(g)),
-              "se dx")
-        return dx, dw1, db1, dw2, db2
+        check(L.ast_mbt_plane_act_f32(6 if ctx.act else 2, ptr(g), None, ptr(gate), ptr(dpool),
+                                      ptr(x) if ctx.act else None, ptr(dx), n * c, h * w, _s(g)), "se dx")
+        return dx, dw1, db1, dw2, db2, None
+
+
+# BatchNorm -> Hardswish, Hardswish -> depthwise conv and Hardswish -> SELayer run fused (no
+# materialised activation); AST_MBT_FUSE=0: the unfused layer chain (A/B runs, bit-identical)
+_FUSE_BN_ACT = os.environ.get("AST_MBT_FUSE", "1") != "0"
 
 
 def block_forward(block, x, x2=None, up: int = 1):
@@ -310,27 +334,42 @@ def block_forward(block, x, x2=None, up: int = 1):
     org_x = x
     h = x
     first_conv = True
-    for layer in block._layers:
+    layers = list(block._layers)
+    skip = False
+    pending_act = 0   # a Hardswish carried into the next depthwise conv / SELayer (not materialised)
+    for i, layer in enumerate(layers):
+        if skip:   # the Hardswish fused into the BatchNorm before it
+            skip = False
+            continue
         if isinstance(layer, nn.ReflectionPad2d):
             continue  # the ratio-1 block's pad: the depthwise kernel pads reflect by (k-1)/2 = 1
         if isinstance(layer, nn.Conv2d):
             if layer.groups > 1:
                 k = layer.kernel_size[0]
-                h = DwConvFn.apply(h, layer.weight, k, layer.stride[0])
+                h = DwConvFn.apply(h, layer.weight, k, layer.stride[0], pending_act)
+                pending_act = 0
             else:
                 h = PwConvFn.apply(h, x2 if first_conv else None, layer.weight)
             first_conv = False
         elif isinstance(layer, nn.BatchNorm2d):
             if layer.training:
-                h = BatchNormTrainFn.apply(h, layer.weight, layer.bias, layer)
+                act = int(i + 1 < len(layers) and isinstance(layers[i + 1], nn.Hardswish) and _FUSE_BN_ACT)
+                h = BatchNormTrainFn.apply(h, layer.weight, layer.bias, layer, act)
+                skip = bool(act)
             else:
                 raise NotImplementedError("eval-mode BatchNorm under autograd: use the inference path "
                                           "(torch.no_grad()) or train mode")
         elif isinstance(layer, nn.Hardswish):
-            h = HardswishFn.apply(h)
+            nxt = layers[i + 1] if i + 1 < len(layers) else None
+            if _FUSE_BN_ACT and (nxt.__class__.__name__ == "SELayer" or
+                                 (isinstance(nxt, nn.Conv2d) and nxt.groups > 1)):
+                pending_act = 1
+            else:
+                h = HardswishFn.apply(h)
         elif layer.__class__.__name__ == "SELayer":
             fc1, fc2 = layer.fc[0], layer.fc[2]
-            h = SEFn.apply(h, fc1.weight, fc1.bias, fc2.weight, fc2.bias)
+            h = SEFn.apply(h, fc1.weight, fc1.bias, fc2.weight, fc2.bias, pending_act)
+            pending_act = 0
         else:
             raise NotImplementedError(f"layer {layer.__class__.__name__} in the training path")
     if block.identity:

@@ -475,6 +475,13 @@ long long ast_mbt_dw_workspace_floats(int n, int c, int h, int wd, int k);
 int ast_mbt_dw_f32(int mode, const float* x, const float* w, const float* g, float* out, int n,
                    int c, int h, int wd, int k, int s, float* workspace, long long workspace_floats,
                    void* stream);
+/* The same with DepthWiseConv's Hardswish -> depthwise conv pair fused (mobilenetv2.py:144-149):
+ * act 1 means the conv's input is hardswish(x) with x the stored pre-activation -- modes 0 and 2
+ * apply it while staging x, mode 1 (x required then) returns the gradient w.r.t. x, taken on
+ * through the Hardswish. Bit-identical to the materialised activation. act 0 = ast_mbt_dw_f32. */
+int ast_mbt_dw_act_f32(int mode, const float* x, const float* w, const float* g, float* out, int n,
+                       int c, int h, int wd, int k, int s, int act, float* workspace,
+                       long long workspace_floats, void* stream);
 
 /* BatchNorm2d in training mode (batch statistics, biased var + eps; running stats updated with
  * momentum and the unbiased variance when run_mean/run_var are given). mean/invstd [c] saved.
@@ -509,6 +516,31 @@ int ast_mbt_bn_bwd_apply_f32(const float* x, const float* dy, int n, int c, long
                              const float* mean, const float* invstd, const float* gamma,
                              const float* sums, const float* inv_count, float* dx, void* stream);
 
+/* The same stages with DepthWiseConv's BatchNorm2d -> Hardswish pair (mobilenetv2.py:122-126,
+ * :150-153) fused: act 1 makes y = hardswish(BN(x)) in the apply pass, and the backward takes dy as
+ * the gradient of that output (through the Hardswish at the recomputed BN output, bit-identical to
+ * the forward's); act 0 is plain BatchNorm (the entries above are these with act 0). beta is needed
+ * by the backward only when act is 1. */
+int ast_mbt_bn_act_fwd_f32(const float* x, int n, int c, long long hw, const float* gamma,
+                           const float* beta, float eps, float momentum, float* mean, float* invstd,
+                           float* run_mean, float* run_var, int act, float* y, float* workspace,
+                           long long workspace_floats, void* stream);
+int ast_mbt_bn_act_apply_f32(const float* x, int n, int c, long long hw, const float* mean,
+                             const float* invstd, const float* gamma, const float* beta, int act, float* y,
+                             void* stream);
+int ast_mbt_bn_act_bwd_f32(const float* x, const float* dy, int n, int c, long long hw,
+                           const float* mean, const float* invstd, const float* gamma, const float* beta,
+                           int act, float* dgamma, float* dbeta, float* dx, float* workspace,
+                           long long workspace_floats, void* stream);
+int ast_mbt_bn_act_bwd_sums_f32(const float* x, const float* dy, int n, int c, long long hw,
+                                const float* mean, const float* invstd, const float* gamma,
+                                const float* beta, int act, float* workspace, long long workspace_floats,
+                                float* sums, void* stream);
+int ast_mbt_bn_act_bwd_apply_f32(const float* x, const float* dy, int n, int c, long long hw,
+                                 const float* mean, const float* invstd, const float* gamma,
+                                 const float* beta, int act, const float* sums, const float* inv_count,
+                                 float* dx, void* stream);
+
 /* op 0 y = hardswish(a); 1 y = hardswish'(a) * b; 2 y = a + b; 3 y = nearest-upsample x2 of a
  * (n planes of h x w); 4 its backward (a = grad of the 2h x 2w planes). */
 int ast_mbt_eltwise_f32(int op, const float* a, const float* b, float* y, long long n, int h,
@@ -518,6 +550,12 @@ int ast_mbt_eltwise_f32(int op, const float* a, const float* b, float* y, long l
  * 2 out = x * gate[p] (+ gadd[p]) over planes of hw elements. */
 int ast_mbt_plane_f32(int op, const float* x, const float* y, const float* gate, const float* gadd,
                       float* out, long long planes, long long hw, void* stream);
+/* ops 0-2 as above, plus the Hardswish -> SELayer pair over the stored pre-activation
+ * (mobilenetv2.py:151-156): 3 out[p] = mean(hardswish(x[p])); 4 out[p] = sum(x[p] * hardswish(y[p]));
+ * 5 out = hardswish(x) * gate[p]; 6 out = hardswish'(a) * (x * gate[p] + gadd[p]) (a: the
+ * pre-activation). Bit-identical to the materialised activation. */
+int ast_mbt_plane_act_f32(int op, const float* x, const float* y, const float* gate, const float* gadd,
+                          const float* a, float* out, long long planes, long long hw, void* stream);
 
 /* SELayer MLP (mobilenetv2.py:63-81): hid = relu(W1 pool + b1), z = W2 hid + b2, gate = clamp(z,0,1);
  * backward from dgate: parameter gradients (overwritten, summed over images in image order) and

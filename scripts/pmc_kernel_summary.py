@@ -31,5 +31,7 @@ for kk, d in agg.items():
           f"{m.get('SQ_ACTIVE_INST_MISC', 0) / wc:.2f}  wait-any {m.get('SQ_WAIT_ANY', 0) / wc:.2f}  wait-inst-any "
           f"{m.get('SQ_WAIT_INST_ANY', 0) / wc:.2f}  wait-lds {m.get('SQ_WAIT_INST_LDS', 0) / wc:.2f}")
     print(f"   LDS bank-conflict cycles / LDS active {m.get('SQ_LDS_BANK_CONFLICT', 0) / max(m.get('SQ_LDS_IDX_ACTIVE', 1), 1):.3f}"
-          f"  MFMA busy / GRBM active {m.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / max(m.get('GRBM_GUI_ACTIVE', 1), 1):.3f}"
+          # SQ_VALU_MFMA_BUSY_CYCLES sums every SIMD's MFMA cycles; GRBM_GUI_ACTIVE sums the 8 XCDs'
+          # clocks (MI355X_MICROARCH.md): busy fraction = busy / (GRBM / 8 * 1024 SIMDs)
+          f"  MFMA busy per SIMD-cycle {m.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / max(m.get('GRBM_GUI_ACTIVE', 1) / 8 * 1024, 1):.3f}"
           f"  FETCH_SIZE {m.get('FETCH_SIZE', 0):.4g} KB  WRITE_SIZE {m.get('WRITE_SIZE', 0):.4g} KB")
