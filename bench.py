@@ -177,8 +177,8 @@ def ae_train_bench(args, dev, rank, world):
         "roofline": {"bound": "mfma", "kernel": "loss-network conv3x3 fwd/dgrad launches of a step (split-bf16)",
                      "achieved": tf, "peak": PEAK_SPLIT_BF16_TF, "unit": "TFLOP/s", "frac": tf / PEAK_SPLIT_BF16_TF,
                      "fp32_mfma_peak": PEAK_FP32_MFMA_TF, "frac_of_fp32_mfma_peak": tf / PEAK_FP32_MFMA_TF,
-                     "traffic": None, "mfma_share_of_step": ms / args.steps / (elapsed / steps_timed * 1e3),
-                     "timing_source": "HIP events around each launch of 3 eager steps of the same shapes"},
+                     "traffic": None, "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3),
+                     "timing_source": "HIP events around each launch of the timed steps"},
         "kernels_ms_per_step": {k: round(m / args.steps, 4) for k, (f, m, c) in sorted(fam.items())},
         "mbgemm_tflops": (fam["mbgemm"][0] / (fam["mbgemm"][1] * 1e-3) / 1e12) if "mbgemm" in fam else None,
     }
