@@ -25,6 +25,19 @@ struct EdArgs {
   int tiles_x, tiles_y;
   int slots;         // output tiles per image (set by the launcher)
   long long* plan;   // non-null: the launcher only stores its slot count here and launches nothing
+  int nod;           // pool-only pass of the fused block pair: SE-pool sums, no D (v4 k3 stride 1 only)
+};
+
+// The recompute-and-project pass of the fused block pair (expand_dw_pw4_kernel, mb_ed4.hip): the
+// expand + depthwise of EdArgs recomputed per output row, the SE-gated pw-linear conv applied from
+// registers/LDS, out = wg[n] . D + b2 (+ res); D never reaches HBM.
+struct EdpwArgs {
+  EdArgs e;           // x1, n, cin, h, w, ho, wo, w1, b1, hid, cin_pad, wdw, bdw (d, pool unused)
+  const void* wg;     // [n][cout_pad][hid_pad] bf16 (ast_mb_se_fold)
+  const float* b2;    // [cout] or null
+  const void* res;    // [n][cout][ho][wo] or null (identity blocks)
+  void* out;          // [n][cout][ho][wo]
+  int cout, cout_pad, hid_pad;
 };
 
 // The launchers' plan-mode exit: the slot count of the launch that would run.
@@ -41,5 +54,9 @@ inline bool ed_plan(EdArgs& a, long long slots) {
 // {16..96, 128}, stride 2 with cin_pad <= 64 and even wo): returns AST_E_UNSUPPORTED when the shape
 // is outside that set (the caller falls back to v3 / v1).
 int launch_ed4(EdArgs a, int k, int stride, hipStream_t st);
+
+// 1 if launch_edpw4 runs this block shape (bf16, k 3, stride 1, no upsample, c1 == cin), else 0.
+int edpw4_supported(int cin_pad, int hid, int cout, int k, int stride, int up, int ho, int wo);
+int launch_edpw4(const EdpwArgs& a, hipStream_t st);
 
 }  // namespace ast_mb

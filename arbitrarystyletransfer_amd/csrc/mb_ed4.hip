@@ -79,8 +79,13 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 // an identity B (exact: bf16 x 1.0 accumulated once in fp32), which is the transposition into the
 // lane-per-channel layout; no Hardswish before the depthwise. UP = 2 resolves the nearest upsample
 // in the gather (reflect on the upsampled grid, then halve).
-template <int K, int KS, int TH, int PD, bool VEC, bool WG4, bool R1 = false, int UP = 1>
-__global__ __launch_bounds__(WG4 ? 64 * ED4_WGN : 64, (K == 5 && KS >= 6) ? 1 : 2) void expand_dw4_kernel(EdArgs a, int strips, int bands, int ncb, int total) {
+// NOD (pool-only pass of the fused block pair, see expand_dw_pw4_kernel): the same row pipeline and SE
+// pool sums, no D stores.
+#ifndef ED4_K5_WPE
+#define ED4_K5_WPE 2  // minimum waves per SIMD of the k5 kernels with cin_pad <= 48 (A/B builds)
+#endif
+template <int K, int KS, int TH, int PD, bool VEC, bool WG4, bool R1 = false, int UP = 1, bool NOD = false>
+__global__ __launch_bounds__(WG4 ? 64 * ED4_WGN : 64, (K == 5 && KS >= 6) ? 1 : (K == 5 && KS <= 3) ? ED4_K5_WPE : 2) void expand_dw4_kernel(EdArgs a, int strips, int bands, int ncb, int total) {
   constexpr int P = (K - 1) / 2, NJ = TH + K - 1, OW = 28, SP = 40;  // SP: staging row pitch (bf16)
   constexpr int NW = ED4_WGN, CPR = NW * OW / 8;  // WG4: strips per workgroup, 16-byte chunks per row
   constexpr int GP = NW * OW + 8;  // WG4 staging row pitch (bf16): 16-byte aligned rows
@@ -173,6 +178,7 @@ __global__ __launch_bounds__(WG4 ? 64 * ED4_WGN : 64, (K == 5 && KS >= 6) ? 1 : 
       }
     }
     psum += rowv ? t : 0.f;
+    if constexpr (NOD) return;
     unsigned pk[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -297,6 +303,15 @@ int launch_ks(EdArgs a, hipStream_t st) {
   const int64_t total = (int64_t)ncb * strips * bands * a.n;
   if (total > 0x7ffffff0LL) return AST_E_SHAPE;
   const int64_t grid = (total + 7) / 8 * 8;
+  if constexpr (!R1 && UP == 1 && K == 3) {
+    if (a.nod) {  // pool-only pass of the fused pair: per-wave strips, no D stores
+      if (ed_plan(a, (int64_t)bands * strips)) return 0;
+      hipLaunchKernelGGL((expand_dw4_kernel<K, KS, TH, PD, true, false, false, 1, true>), dim3((unsigned)grid), dim3(64), 0,
+                         st, a, strips, bands, ncb, (int)total);
+      return (int)hipGetLastError();
+    }
+  }
+  if (a.nod) return AST_E_UNSUPPORTED;
   // WG4 for k = 3 only: measured 3.3 -> 2.9 ms on the 16->96 block at 1024^2, while the k5 blocks
   // lose 10-50% to the per-row workgroup barrier (their rows are longer and less uniform)
   if (ED4_WG4 && K == 3 && a.wo % 8 == 0) {  // WG4: 4 strips per workgroup, 16-byte D stores
@@ -502,9 +517,213 @@ int launch_s2(EdArgs a, hipStream_t st) {
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Fused block pair, pass 2: expand + depthwise recomputed, SE-gated pw-linear conv in the kernel
+// ------------------------------------------------------------------------------------------------
+// Materialising the depthwise output D costs a hidden-width write and read per block (the pw kernel
+// re-reads it), yet the SE gate needs the whole image pooled before the pw-linear conv can run. The
+// pair: pass 1 is expand_dw4_kernel<.., NOD> (pool sums only, no D), ast_mb_se_fold folds the gate
+// into wg[n], and this pass recomputes expand + depthwise and applies wg directly. A workgroup is one
+// strip x band of one image:
+//  * NCB compute waves: wave cb computes hidden channels 32 cb .. 32 cb + 31 exactly as
+//    expand_dw4_kernel (same instructions, same rounding) and writes each finished output row to LDS
+//    as bf16 [channel][32 columns] -- the values D would hold;
+//  * one GEMM wave (wave NCB) consumes row r while the compute waves produce row r + 1 (two row
+//    images; one workgroup barrier per row orders both the hand-over and the reuse): the pw GEMM
+//    out[co][px] = sum_c wg[n][co][c] D[c][px] as 16 x 16 tiles on v_mfma_f32_16x16x32_bf16 with
+//    pw_kernel's operand layout and chunk order (A = wg[n] from LDS, B through ds_read_b64_tr_b16),
+//    then + b2 (+ residual) as pw_kernel does: the output is bit-identical to expand_dw4 + se_fold +
+//    pw. 28 of the 32 columns are stored.
+// HBM traffic per block: x twice (both passes) and out once, against x, D written, D read and out.
+template <int KS, int NCB, int NCO>
+__global__ __launch_bounds__(64 * (NCB + 1)) __attribute__((amdgpu_waves_per_eu(3))) void expand_dw_pw4_kernel(
+    EdpwArgs pa, int strips, int bands, int total) {
+  constexpr int K = 3, P = 1, TH = ED4_TH, NJ = TH + K - 1, OW = 28, DP = 48;  // DP: D image row pitch (bf16)
+  constexpr int NT = 2 * NCO;  // 16 x 16 output tiles per row: (output-channel block, pixel half)
+  // wg[n] in LDS, row pitch = 8 (mod 128) elements: the A fragments' 8-byte reads (16 rows x 2
+  // k-groups per half-wave) hit distinct banks
+  constexpr int WP = (NCB * 32 + 127) / 128 * 128 + 8;
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  __shared__ __align__(16) bf16 dimg[2][NCB * 32 * DP];
+  __shared__ __align__(16) bf16 wsm[NCO * 16 * WP];
+  const EdArgs& a = pa.e;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, cb = threadIdx.x >> 6;
+  const int per = (total + 7) >> 3;
+  const int L = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (L >= total) return;
+  const int s = L % strips;
+  const int rest = L / strips;
+  const int band = rest % bands;
+  const int n = rest / bands;
+  const int x0 = s * OW - 2, y0 = band * TH;
+  {
+    const bf16* wn = reinterpret_cast<const bf16*>(pa.wg) + (int64_t)n * pa.cout_pad * pa.hid_pad;
+    for (int e = threadIdx.x; e < NCO * 16 * NCB * 4; e += 64 * (NCB + 1)) {  // 8-element pieces
+      const int row = e / (NCB * 4), c8 = e - row * (NCB * 4);
+      *reinterpret_cast<u32x4*>(wsm + row * WP + 8 * c8) =
+          *reinterpret_cast<const u32x4*>(wn + (int64_t)row * pa.hid_pad + 8 * c8);
+    }
+  }  // (ordered before the first GEMM by the first row barrier)
+
+  if (cb == NCB) {  // ---- GEMM wave ----
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int64_t plane_o = (int64_t)a.ho * a.wo;
+    const int orange = (int)(2 * pa.cout * plane_o);
+    const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<bf16*>(pa.out) + (int64_t)n * pa.cout * plane_o, 0, orange, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16*>(reinterpret_cast<const bf16*>(pa.res ? pa.res : pa.out)) + (int64_t)n * pa.cout * plane_o,
+        0, pa.res ? orange : 0, 0x00020000);
+    constexpr unsigned kDrop = 0x80000000u;
+    float bco[NCO][4];
+#pragma unroll
+    for (int m = 0; m < NCO; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = 16 * m + 4 * g + j;
+        bco[m][j] = (pa.b2 && co < pa.cout) ? pa.b2[co] : 0.f;
+      }
+    for (int orow = 0; orow < TH; ++orow) {
+      const int oy = y0 + orow;
+      const bool rowv = oy < a.ho;
+      unsigned off[NT][4];
+      unsigned short rv[NT][4];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int px = (t & 1) * 16 + (lane & 15), ox = x0 + px;
+        const bool ok = rowv && px >= 2 && px < 2 + OW && ox < a.wo;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int co = t / 2 * 16 + 4 * g + j;
+          off[t][j] = (ok && co < pa.cout) ? (unsigned)(2 * (co * plane_o + (int64_t)oy * a.wo + ox)) : kDrop;
+          rv[t][j] = pa.res ? __builtin_amdgcn_raw_buffer_load_b16(rr, (int)off[t][j], 0, 0) : (unsigned short)0;
+        }
+      }
+      lds_barrier();  // row orow's image is complete
+      const bf16* img = dimg[orow & 1];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int col = (t & 1) * 16 + 4 * p4;
+        const bf16* wr = wsm + (t / 2 * 16 + (lane & 15)) * WP + 4 * g;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < NCB; ++kc) {
+          const s16x4 alo = *reinterpret_cast<const s16x4*>(wr + 32 * kc);
+          const s16x4 ahi = *reinterpret_cast<const s16x4*>(wr + 32 * kc + 16);
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (32 * kc + 4 * g + q4) * DP + col));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (32 * kc + 16 + 4 * g + q4) * DP + col));
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7)),
+              __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7)), acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float o = acc[j] + bco[t / 2][j];
+          if (pa.res) o = o + (float)__builtin_bit_cast(bf16, rv[t][j]);
+          __builtin_amdgcn_raw_buffer_store_b16(bf16_bits(o), orr, (int)off[t][j], 0, 0);
+        }
+      }
+    }
+    return;
+  }
+
+  // ---- compute waves: expand_dw4_kernel's row pipeline for channels 32 cb .. 32 cb + 31 ----
+  const int ch = cb * 32 + r;
+  const bool chv = ch < a.hid;
+  float wk[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) wk[i] = chv ? a.wdw[ch * K * K + i] : 0.f;
+  const float bd = chv ? a.bdw[ch] : 0.f, b1 = chv ? a.b1[ch] : 0.f;
+  const int hid16 = (a.hid + 15) / 16 * 16;
+  bf16x8 bw[KS];
+#pragma unroll
+  for (int q = 0; q < KS; ++q)
+    bw[q] = ch < hid16 ? *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.w1) +
+                                                          (int64_t)ch * a.cin_pad + 16 * q + 8 * h)
+                       : bf16x8{};
+  const int pc = 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3);
+  const int gx = refl(x0 + pc, a.wd);
+  const int hw2 = 2 * a.h * a.w;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(reinterpret_cast<const bf16*>(a.x1) + (int64_t)n * a.cin * (hw2 / 2)), 0, a.cin * hw2,
+      0x00020000);
+  unsigned xraw[KS][8];
+  auto load_row = [&](int j) {
+    const int vrow = 8 * h * hw2 + 2 * (refl(y0 - P + j, a.hd) * a.w + gx);
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xraw[q][e] = __builtin_amdgcn_raw_buffer_load_b16(xr, vrow + (16 * q + e) * hw2, 0, 0);
+  };
+  auto finish = [&](int orow, const float* v, bool live) {
+    if (!live) return;  // uniform over the workgroup
+    float y[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) y[i] = hswish_fast(v[i]);
+    unsigned pk[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      pk[i] = (unsigned)bf16_bits(y[2 * i]) | ((unsigned)bf16_bits(y[2 * i + 1]) << 16);
+    u32x4* dw = reinterpret_cast<u32x4*>(dimg[orow & 1] + ch * DP + 16 * h);
+    dw[0] = u32x4{pk[0], pk[1], pk[2], pk[3]};
+    dw[1] = u32x4{pk[4], pk[5], pk[6], pk[7]};
+    lds_barrier();  // hand the row to the GEMM wave (which has finished the row two back)
+  };
+
+  static_assert(NJ % K == 0, "TH + K - 1 must be a multiple of K");
+  float acc[K][16];
+  load_row(0);
+  for (int jb = 0; jb < NJ; jb += K) {
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+      const int j = jb + u;
+      f32x16 c;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) c[i] = b1;
+#pragma unroll
+      for (int q = 0; q < KS; ++q) {
+        u32x4 f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f[e] = (xraw[q][2 * e] & 0xffffu) | (xraw[q][2 * e + 1] << 16);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f), bw[q], c, 0, 0, 0);
+      }
+      load_row(j + 1);
+      float e[20];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) e[2 + i] = hswish_fast(c[i]);
+      const float r0 = __shfl_xor(h ? e[2] : e[16], 32, 64), r1 = __shfl_xor(h ? e[3] : e[17], 32, 64);
+      e[0] = r0;
+      e[1] = r1;
+      e[18] = r0;
+      e[19] = r1;
+#pragma unroll
+      for (int ky = K - 1; ky >= 0; --ky) {
+        const int orow = j - ky;
+        const int slot = ((u - ky) % K + K) % K;
+        const bool live = orow >= 0 && orow < TH;
+        if (live) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            float v = ky == 0 ? bd : acc[slot][i];
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) v = fmaf(wk[ky * K + kx], e[i + 2 - P + kx], v);
+            acc[slot][i] = v;
+          }
+        }
+        if (ky == K - 1) finish(orow, acc[slot], live);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 int launch_ed4(EdArgs a, int k, int stride, hipStream_t st) {
+  if (a.nod && (!a.w1 || stride != 1 || k != 3)) return AST_E_UNSUPPORTED;
   if (a.c1 != a.cin || (a.w1 && a.cin_pad % 16 != 0) || (int64_t)a.cin_pad * 2 * a.h * a.w >= 0x7fffffffLL ||
       (int64_t)a.hid * 2 * a.ho * a.wo >= 0x7fffffffLL)
     return AST_E_UNSUPPORTED;
@@ -527,6 +746,46 @@ int launch_ed4(EdArgs a, int k, int stride, hipStream_t st) {
   }
   if (k == 3) return launch_k<3>(a, st);
   if (k == 5) return launch_k<5>(a, st);
+  return AST_E_UNSUPPORTED;
+}
+
+
+// (cin_pad / 16, hidden channel blocks of 32, output channel blocks of 16) instantiated for the
+// fused pair: the stride-1 k3 expand blocks of config 5 with narrow inputs (16 -> 96 -> 16,
+// 24 -> 144 -> 24 | 16)
+#define EDPW_SHAPES(X) X(1, 3, 1) X(2, 5, 2) X(2, 5, 1)
+
+int edpw4_supported(int cin_pad, int hid, int cout, int k, int stride, int up, int ho, int wo) {
+  if (k != 3 || stride != 1 || up != 1 || ho < 2 || wo < 2) return 0;
+  const int ks = cin_pad / 16, ncb = (hid + 31) / 32, nco = (cout + 15) / 16;
+#define EDPW_CASE(KS_, NCB_, NCO_) if (ks == KS_ && ncb == NCB_ && nco == NCO_) return 1;
+  EDPW_SHAPES(EDPW_CASE)
+#undef EDPW_CASE
+  return 0;
+}
+
+int launch_edpw4(const EdpwArgs& pa, hipStream_t st) {
+  const EdArgs& a = pa.e;
+  if (!a.w1 || a.c1 != a.cin || a.hd != a.h || a.wd != a.w || a.ho != a.h || a.wo != a.w || a.cin_pad % 16 != 0)
+    return AST_E_UNSUPPORTED;
+  if (!edpw4_supported(a.cin_pad, a.hid, pa.cout, 3, 1, 1, a.ho, a.wo)) return AST_E_UNSUPPORTED;
+  if (pa.hid_pad != (a.hid + 31) / 32 * 32 || pa.cout_pad != (pa.cout + 15) / 16 * 16) return AST_E_SHAPE;
+  if ((int64_t)a.cin_pad * 2 * a.h * a.w >= 0x7fffffffLL || (int64_t)pa.cout * 2 * a.ho * a.wo >= 0x7fffffffLL)
+    return AST_E_UNSUPPORTED;
+  constexpr int TH = ED4_TH;
+  const int strips = (a.wo + 27) / 28, bands = (a.ho + TH - 1) / TH;
+  const int64_t total = (int64_t)strips * bands * a.n;
+  if (total > 0x7ffffff0LL) return AST_E_SHAPE;
+  const unsigned grid = (unsigned)((total + 7) / 8 * 8);
+  const int ks = a.cin_pad / 16, ncb = (a.hid + 31) / 32, nco = (pa.cout + 15) / 16;
+#define EDPW_CASE(KS_, NCB_, NCO_)                                                                       \
+  if (ks == KS_ && ncb == NCB_ && nco == NCO_) {                                                         \
+    hipLaunchKernelGGL((expand_dw_pw4_kernel<KS_, NCB_, NCO_>), dim3(grid), dim3(64 * (NCB_ + 1)), 0, st, pa, strips, \
+                       bands, (int)total);                                                               \
+    return (int)hipGetLastError();                                                                       \
+  }
+  EDPW_SHAPES(EDPW_CASE)
+#undef EDPW_CASE
   return AST_E_UNSUPPORTED;
 }
 

@@ -112,6 +112,7 @@ __device__ __forceinline__ void load8(const bf16* s, float* v) {
 // expand + depthwise (+ SE pool sums)
 // ------------------------------------------------------------------------------------------------
 using ast_mb::EdArgs;  // mb_common.h (shared with mb_ed4.hip)
+using ast_mb::EdpwArgs;
 
 constexpr int kChunk = 16;  // hidden channels per LDS chunk
 
@@ -1621,8 +1622,9 @@ int dispatch_ed(EdArgs a, int k, int s, int up, bool expand, hipStream_t st) {
   if (sizeof(T) == 2 && (up == 1 || !expand) && g_ed_version >= 4 && a.c1 == a.cin &&
       (int64_t)a.cin_pad * 2 * a.h * a.w < 0x7fffffffLL) {
     const int r = ast_mb::launch_ed4(a, k, s, st);
-    if (r != AST_E_UNSUPPORTED) return r;
+    if (r != AST_E_UNSUPPORTED || a.nod) return r;
   }
+  if (a.nod) return AST_E_UNSUPPORTED;  // pool-only: the v4 kernels only
   if (sizeof(T) == 2 && s == 1 && up == 1 && expand && g_ed_version >= 3) {
     const int r = k == 3 ? launch_ed3<3>(a, st) : k == 5 ? launch_ed3<5>(a, st) : AST_E_UNSUPPORTED;
     if (r != AST_E_UNSUPPORTED) return r;
@@ -1754,6 +1756,7 @@ extern "C" {
 
 long long ast_mb_expand_dw_workspace_floats(int dtype, int has_x2, int c1, int n, int cin, int h, int w, int up,
                                             int expand, int hid, int cin_pad, int k, int stride, int ho, int wo) {
+  // (the pool-only form, d == NULL, never needs more slots than the D-writing form planned here)
   static const char dummy = 0;  // stand-in pointers: the plan only looks at their presence
   EdArgs a;
   if (ed_setup(dtype, &dummy, has_x2 ? &dummy : nullptr, c1, n, cin, h, w, up, expand ? &dummy : nullptr, hid,
@@ -1769,10 +1772,11 @@ int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, i
                      const void* w1p, const float* b1, int hid, int cin_pad, const float* wdw, const float* bdw,
                      int k, int stride, void* d, float* pool, int ho, int wo, float* workspace,
                      long long workspace_floats, void* stream) {
-  if (!x1 || !wdw || !bdw || !d || !pool || !workspace) return AST_E_NULLPTR;
+  if (!x1 || !wdw || !bdw || !pool || !workspace) return AST_E_NULLPTR;
   if (w1p && !b1) return AST_E_NULLPTR;
   EdArgs a;
   if (const int e = ed_setup(dtype, x1, x2, c1, n, cin, h, w, up, w1p, hid, cin_pad, k, stride, ho, wo, &a)) return e;
+  a.nod = d == nullptr;  // pool-only pass of the fused pair
   hipStream_t st = (hipStream_t)stream;
   long long slots = 0;
   a.plan = &slots;
@@ -1788,6 +1792,33 @@ int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, i
   if (const int e = ed_dispatch(dtype, a, k, stride, up, st)) return e;
   // pool[n][c] = the channel's tile sums in tile order
   return (int)ast_det::reduce_rows(workspace, (int64_t)n * hid, (int)slots, pool, st);
+}
+
+int ast_mb_expand_dw_pw_supported(int dtype, int has_x2, int cin, int cin_pad, int hid, int cout, int k, int stride,
+                                  int up, int ho, int wo) {
+  if (dtype != 1 || has_x2 || cin <= 0 || cin_pad < cin || cin_pad % 16) return 0;
+  return ast_mb::edpw4_supported(cin_pad, hid, cout, k, stride, up, ho, wo);
+}
+
+int ast_mb_expand_dw_pw(int dtype, const void* x, int n, int cin, int h, int w, const void* w1p, const float* b1,
+                        int hid, int cin_pad, const float* wdw, const float* bdw, int k, const void* wg, int cout,
+                        int cout_pad, int hid_pad, const float* b2, const void* res, void* out, void* stream) {
+  if (!x || !w1p || !b1 || !wdw || !bdw || !wg || !out) return AST_E_NULLPTR;
+  if (n <= 0 || cout <= 0) return AST_E_SHAPE;
+  if (!ast_mb_expand_dw_pw_supported(dtype, 0, cin, cin_pad, hid, cout, k, 1, 1, h, w)) return AST_E_UNSUPPORTED;
+  EdpwArgs pa{};
+  if (const int e = ed_setup(dtype, x, nullptr, cin, n, cin, h, w, 1, w1p, hid, cin_pad, k, 1, h, w, &pa.e)) return e;
+  pa.e.b1 = b1;
+  pa.e.wdw = wdw;
+  pa.e.bdw = bdw;
+  pa.wg = wg;
+  pa.b2 = b2;
+  pa.res = res;
+  pa.out = out;
+  pa.cout = cout;
+  pa.cout_pad = cout_pad;
+  pa.hid_pad = hid_pad;
+  return ast_mb::launch_edpw4(pa, (hipStream_t)stream);
 }
 
 int ast_mb_se_fold(int dtype, const float* pool, int n, int hid, long long hw, const float* fc1w,

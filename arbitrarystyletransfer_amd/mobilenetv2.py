@@ -16,6 +16,7 @@ and accumulation are fp32.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -31,6 +32,10 @@ DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1}
 # once, write its output once) — bench.py's config-5 roofline denominator.
 IO_TRACE = None
 DW_TRACE = None   # bench.py: per expand_dw launch, the depthwise multiply-adds (VALU work)
+# AST_MB_EDPW=1: the fused block pair (ast_mb_expand_dw_pw: no hidden-width tensor in memory) for
+# the shapes it supports. Off by default: bit-identical, but measured 3% slower on the config-5 step
+# than expand_dw + se_fold + pw ("Fused block pair").
+FUSED_PAIR = os.environ.get("AST_MB_EDPW", "0") == "1"
 
 
 def _trace_io(nbytes: int) -> None:
@@ -75,7 +80,7 @@ def _expand_dw(dt, x1, x2, c1, n, cin, h, w, up, w1p, b1, hid, cin_pad, wd, bd, 
     nws = _ED_WS.get(key)
     if nws is None:
         nws = _ED_WS[key] = int(lib().ast_mb_expand_dw_workspace_floats(*(int(v) for v in key)))
-    ws = workspace(nws, d.device)
+    ws = workspace(nws, pool.device)
     return lib().ast_mb_expand_dw(DTYPE_CODE[dt], ptr(x1), ptr(x2), c1, n, cin, h, w, up, ptr(w1p), ptr(b1), hid,
                                   cin_pad, ptr(wd), ptr(bd), k, s, ptr(d), ptr(pool), ho, wo, ptr(ws), ws.numel(), st)
 
@@ -261,6 +266,10 @@ class DepthWiseConv(nn.Module):
         self._pl, self._plan_stamp = p, stamp
         return p
 
+    def _fused_ok(self, dt, cin, cin_pad, hid, cout, k, s, ho, wo):
+        """The fused block pair (ast_mb_expand_dw_pw) runs this block shape."""
+        return bool(lib().ast_mb_expand_dw_pw_supported(DTYPE_CODE[dt], 0, cin, cin_pad, hid, cout, k, s, 1, ho, wo))
+
     # -- forward --------------------------------------------------------------------------------
     def forward(self, x, x2=None):
         return self.run(x, x2, 1)
@@ -298,9 +307,11 @@ class DepthWiseConv(nn.Module):
         hid, cout = self.hidden_dim, self.oup
         dev, st = x.device, stream_ptr(x.device)
         es = x.element_size()
-        d = torch.empty((n, hid, ho, wo), device=dev, dtype=dt)
+        fused = (FUSED_PAIR and x2 is None and up == 1 and p.w1p is not None
+                 and self._fused_ok(dt, cin, p.cin_pad, hid, cout, k, s, ho, wo))
+        d = None if fused else torch.empty((n, hid, ho, wo), device=dev, dtype=dt)
         pool = torch.empty((n, hid), device=dev, dtype=torch.float32)
-        nb1 = es * (n * cin * h * w + d.numel())
+        nb1 = es * (n * cin * h * w + (d.numel() if d is not None else 0))
         tag = f"mb expand_dw k{k}s{s}{' up' if up == 2 else ''} {cin}->{hid} {ho}x{wo}"
         if (dt == torch.bfloat16 and p.w1p is not None and p.cin_pad >= 256 and p.cin_pad % 32 == 0
                 and hid % 128 == 0 and s == 1 and up == 1 and k == 3):
@@ -315,6 +326,13 @@ class DepthWiseConv(nn.Module):
                              lambda: _expand_dw(dt, hmid, None, hid, n, hid, h, w, 1, None, None, hid, 0, p.wd, p.bd,
                                                 k, s, d, pool, ho, wo, st)),
                   "DepthWiseConv dw")
+        elif fused:
+            # the fused pair: pool-only pass (no D), SE fold, then expand + depthwise recomputed with
+            # the gated pw-linear conv applied in the kernel (csrc/mb_ed4.hip expand_dw_pw4_kernel)
+            check(ops._timed(f"mb expand_dw k{k}s{s} pool {cin}->{hid} {ho}x{wo}", -es * n * cin * h * w, dev,
+                             lambda: _expand_dw(dt, x, None, c1, n, cin, h, w, 1, p.w1p, p.b1, hid, p.cin_pad, p.wd,
+                                                p.bd, k, s, None, pool, ho, wo, st)),
+                  "DepthWiseConv pool pass")
         else:
             check(ops._timed(tag, -nb1, dev,
                              lambda: _expand_dw(dt, x, x2, c1, n, cin, h, w, up, p.w1p, p.b1, hid, p.cin_pad, p.wd,
@@ -329,6 +347,14 @@ class DepthWiseConv(nn.Module):
         if DW_TRACE is not None:   # depthwise FMAs of the expand_dw launch (bench.py's VALU figure)
             DW_TRACE.append(n * hid * ho * wo * k * k)
         res = x if self.identity else None
+        if fused:
+            nb3 = es * (n * cin * h * w + out.numel() + (res.numel() if res is not None else 0))
+            check(ops._timed(f"mb expand_dw_pw k{k}s{s} {cin}->{hid}->{cout} {ho}x{wo}", -nb3, dev,
+                             lambda: lib().ast_mb_expand_dw_pw(
+                                 DTYPE_CODE[dt], ptr(x), n, cin, h, w, ptr(p.w1p), ptr(p.b1), hid, p.cin_pad,
+                                 ptr(p.wd), ptr(p.bd), k, ptr(wg), cout, p.cout_pad, p.hid_pad, ptr(p.b2), ptr(res),
+                                 ptr(out), st)), "DepthWiseConv fused expand+dw+pw")
+            return out
         nb2 = es * (d.numel() + out.numel() + (res.numel() if res is not None else 0))
         check(ops._timed(f"mb pw {hid}->{cout} {ho}x{wo}", -nb2, dev, lambda: lib().ast_mb_pw(
             DTYPE_CODE[dt], ptr(d), n, hid, p.hid_pad, ho, wo, ptr(wg), p.cout_pad * p.hid_pad, ptr(p.b2), cout,

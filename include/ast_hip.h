@@ -290,13 +290,29 @@ int ast_adam_step_sched_f32(const void* dev_table, int ntensors, long long nchun
  * Upsample (models.py:264-266) to x first. x2 != NULL feeds channels [c1, cin) from a second
  * tensor (the torch.cat before ada_out, models.py:335). workspace: the floats returned by
  * ast_mb_expand_dw_workspace_floats for the same arguments (has_x2 = x2 != NULL,
- * expand = w1p != NULL); <= 0 means the shape is unsupported. */
+ * expand = w1p != NULL); <= 0 means the shape is unsupported. d == NULL is the pool-only pass
+ * of the fused block pair (ast_mb_expand_dw_pw): pool is made, nothing else is written (bf16, k 3,
+ * stride 1, expand blocks; AST_E_UNSUPPORTED elsewhere). */
 long long ast_mb_expand_dw_workspace_floats(int dtype, int has_x2, int c1, int n, int cin, int h, int w, int up,
                                             int expand, int hid, int cin_pad, int k, int stride, int ho, int wo);
 int ast_mb_expand_dw(int dtype, const void* x1, const void* x2, int c1, int n, int cin, int h, int w,
                      int up, const void* w1p, const float* b1, int hid, int cin_pad,
                      const float* wdw, const float* bdw, int k, int stride, void* d, float* pool,
                      int ho, int wo, float* workspace, long long workspace_floats, void* stream);
+
+/* The fused block pair (DepthWiseConv.forward, mobilenetv2.py:153-165, without its hidden-width
+ * tensor in memory): after ast_mb_expand_dw(d = NULL) made pool and ast_mb_se_fold made wg, this
+ * recomputes the expand + depthwise of x and applies wg directly: out[n][co] = sum_c wg[n][co][c] *
+ * D[n][c] + b2[co] (+ res[n][co]) in bf16, bit-identical to ast_mb_expand_dw + ast_mb_pw. Shapes:
+ * ast_mb_expand_dw_pw_supported (1 = supported: bf16, k 3, stride 1, up 1, no x2, and the
+ * (cin_pad, hid, cout) combinations instantiated). b2 and res may be NULL; hid_pad =
+ * round_up(hid, 32), cout_pad = round_up(cout, 16). */
+int ast_mb_expand_dw_pw_supported(int dtype, int has_x2, int cin, int cin_pad, int hid, int cout, int k,
+                                  int stride, int up, int ho, int wo);
+int ast_mb_expand_dw_pw(int dtype, const void* x, int n, int cin, int h, int w, const void* w1p,
+                        const float* b1, int hid, int cin_pad, const float* wdw, const float* bdw, int k,
+                        const void* wg, int cout, int cout_pad, int hid_pad, const float* b2,
+                        const void* res, void* out, void* stream);
 
 /* SELayer (mobilenetv2.py:63-81) on the pooled sums (mean = pool / hw), folded into the pw-linear
  * weights w2 [cout][hid]: wg[n][co][c] = w2[co][c] * gate[n][c], written as dtype

@@ -37,7 +37,10 @@ def pair(*shape, scale=1.0):
 
 
 @pytest.mark.parametrize("split,shape,cout", [(False, (2, 24, 9, 13), 40), (True, (2, 24, 9, 13), 40),
-                                              (False, (3, 96, 5, 5), 130), (True, (4, 40, 20, 20), 72)])
+                                              (False, (3, 96, 5, 5), 130), (True, (4, 40, 20, 20), 72),
+                                              # wide M, long K, odd K, large planes
+                                              (False, (2, 16, 40, 64), 144), (False, (1, 144, 33, 32), 24),
+                                              (False, (2, 17, 8, 12), 33), (True, (2, 96, 16, 16), 260)])
 def test_pw_conv(split, shape, cout):
     torch.manual_seed(0)
     xc, xg = pair(*shape)

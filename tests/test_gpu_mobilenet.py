@@ -89,6 +89,38 @@ def test_block_bf16(case, hip_device):
     assert rel_inf(y, ref) <= BF16_BLOCK_TOL
 
 
+FUSED_CASES = [
+    # inp, oup, expand, use_norm, (n, h, w): the stride-1 k3 expand blocks of the fused pair
+    (16, 16, 6, True, (2, 20, 36)),
+    (16, 16, 6, False, (1, 70, 97)),     # 3 bands of rows, ragged last strip
+    (24, 24, 6, False, (2, 33, 57)),
+    (24, 16, 6, True, (1, 64, 64)),      # no residual (cout != cin)
+    (24, 24, 6, False, (1, 5, 7)),       # smaller than one strip and one band
+]
+
+
+@pytest.mark.parametrize("case", FUSED_CASES)
+def test_fused_pair_matches_unfused(case, hip_device, monkeypatch):
+    """The fused block pair (pool-only pass, SE fold, expand + depthwise recomputed with the gated
+    pw-linear conv in the kernel: no hidden-width tensor in HBM) is bit-identical to the
+    expand_dw -> se_fold -> pw chain, and within the bf16 bar of the oracle (mobilenetv2.py:153-165)."""
+    from arbitrarystyletransfer_amd import mobilenetv2 as M
+    inp, oup, t, norm, (n, h, w) = case
+    blk = synth.live_init_(DepthWiseConv(inp, oup, 1, t, kernel_size=3, use_norm=norm), 970 + inp + oup)
+    blk = blk.eval().to(hip_device).to(torch.bfloat16)
+    assert blk._fused_ok(torch.bfloat16, inp, (inp + 15) // 16 * 16, blk.hidden_dim, oup, 3, 1, h, w)
+    x = torch.from_numpy(synth.image(971 + inp, (n, inp, h, w)) * 2 - 0.7).to(hip_device).to(torch.bfloat16)
+    with torch.no_grad():
+        monkeypatch.setattr(M, "FUSED_PAIR", True)
+        y_f = blk(x)
+        monkeypatch.setattr(M, "FUSED_PAIR", False)
+        y_u = blk(x)
+        ref = R.mb_block(x.float().cpu(), cpu_sd(blk), "", inp, oup, 1, t, 3, norm, True)
+    torch.cuda.synchronize()
+    assert torch.equal(y_f, y_u), rel_inf(y_f, y_u)
+    assert rel_inf(y_f, ref) <= BF16_BLOCK_TOL
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_ada_out_split_input_matches_cat(dtype, hip_device):
     blk = synth.live_init_(DepthWiseConv(256, 128, 1, 3, use_norm=False, use_identity=False), 7)

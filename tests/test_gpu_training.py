@@ -244,12 +244,12 @@ def oracle_decoder_gpu_masks(t, dec, d):
     with torch.no_grad():
         h = t.detach()
         for (w, b), (cin, cout, up) in zip(dec, synth.VGG_DECODER_SPEC):
-            pre, _, _ = ops.conv3x3(h, ops.pack_conv3x3(w.detach().to(d)), b.detach().to(d), cout,
+            pre, _, _ = ops.conv3x3(h, ops.pack_conv3x3(w.detach().float().to(d)), b.detach().float().to(d), cout,
                                     upsample=2 if up else 1, pad_mode="reflect", want_pre=True, want_act=False)
             relu = cout != 3
             masks.append((pre > 0).cpu() if relu else None)
             h = torch.relu(pre) if relu else pre
-    h = t.detach().cpu()
+    h = t.detach().cpu().to(dec[0][0].dtype)
     for (w, b), (cin, cout, up), m in zip(dec, synth.VGG_DECODER_SPEC, masks):
         if up:
             h = F.interpolate(h, scale_factor=2, mode="nearest")
@@ -271,9 +271,9 @@ def oracle_lossnet_gpu_routing(x, enc, names, d):
     wanted = set(names)
     route = []
     with torch.no_grad():
-        h = x.detach().to(d)
+        h = x.detach().float().to(d)
         for i, (w, b) in enumerate(enc, start=1):
-            pre, _, _ = ops.conv3x3(h, ops.pack_conv3x3(w.to(d)), b.to(d), w.shape[0], pad_mode="zeros",
+            pre, _, _ = ops.conv3x3(h, ops.pack_conv3x3(w.float().to(d)), b.float().to(d), w.shape[0], pad_mode="zeros",
                                     in_mean=mean if i == 1 else None, in_std=std if i == 1 else None,
                                     want_pre=True, want_act=False)
             act = torch.relu(pre)
@@ -529,35 +529,46 @@ def test_train_step_512_vs_oracle(hip_device):
     for k in ("content_loss", "style_loss", "lf_loss", "tv_loss", "loss"):
         np.testing.assert_allclose(out[k].item(), ref[k].item(), rtol=1e-4, err_msg=k)
     assert rel_inf(out["stylized"], ref["stylized"]) <= 1e-4
-    xs = out["stylized"].detach().cpu().requires_grad_()
     names = R.LOSSNET_LAYERS
-    with torch.no_grad():
-        cm = R.vgg_encoder(content, enc, names)
-        sm = R.vgg_encoder(style, enc, names)
-    tcs = oracle_lossnet_gpu_routing(xs, enc, names, d)
-    cl = sum(R.compute_content_loss(R.mean_variance_norm(a), R.mean_variance_norm(b)) for a, b in zip(tcs, cm))
-    cl = cl + R.compute_content_loss(R.mean_variance_norm(xs), R.mean_variance_norm(content)) * 0.1
-    sl = sum(R.compute_style_loss(a, b) * w for a, b, w in zip(tcs, sm, R.STYLE_WEIGHTS))
-    sl = sl + R.compute_style_loss(xs, style)
-    (1.25 * cl + 0.5 * sl + 0.0006 * R.tv_loss(xs)).backward()
-    del tcs, cm, sm
-    params = [p for wb in dec for p in wb]
-    h = oracle_decoder_gpu_masks(out["t"], dec, d)
-    assert rel_inf(h, xs) <= 1e-4
-    torch.autograd.backward(h, grad_tensors=xs.grad)
-    # 5e-4, not the 64^2 tests' 2e-4: the decoder routing is matched (GPU masks) but the loss
-    # network's ReLU / max-pool routing at 512^2 (100x the pixels, so more near-ties) is the
-    # CPU's own; measured worst 1.3e-4 (fp32 MFMA kernel) / 2.8e-4 (split-bf16 kernel), both the
-    # final conv's bias, a plain sum of dL/dx over all 2 x 512^2 pixels
-    worst = 0.0
-    for i, (gr, p) in enumerate(zip(snap["grads"], params)):
-        e = rel_inf(gr, p.grad)
+
+    def reference_grads(dt):
+        """The oracle's decoder gradients at the GPU's forward point (GPU routing), in dtype dt."""
+        xs = out["stylized"].detach().cpu().to(dt).requires_grad_()
+        e = [(w.to(dt), b.to(dt)) for w, b in enc]
+        dd = [(w.detach().to(dt).requires_grad_(), b.detach().to(dt).requires_grad_()) for w, b in dec]
+        c, s = content.to(dt), style.to(dt)
+        with torch.no_grad():
+            cm = R.vgg_encoder(c, e, names)
+            sm = R.vgg_encoder(s, e, names)
+        tcs = oracle_lossnet_gpu_routing(xs, e, names, d)
+        cl = sum(R.compute_content_loss(R.mean_variance_norm(a), R.mean_variance_norm(b)) for a, b in zip(tcs, cm))
+        cl = cl + R.compute_content_loss(R.mean_variance_norm(xs), R.mean_variance_norm(c)) * 0.1
+        sl = sum(R.compute_style_loss(a, b) * w for a, b, w in zip(tcs, sm, R.STYLE_WEIGHTS))
+        sl = sl + R.compute_style_loss(xs, s)
+        (1.25 * cl + 0.5 * sl + 0.0006 * R.tv_loss(xs)).backward()
+        del tcs, cm, sm
+        h = oracle_decoder_gpu_masks(out["t"], dd, d)
+        assert rel_inf(h, xs) <= 1e-4
+        torch.autograd.backward(h, grad_tensors=xs.grad)
+        return [p for wb in dd for p in wb]
+
+    # The bar is 2e-5 against the float64 evaluation of the same computation (GPU routing); the
+    # CPU's own fp32 evaluation is reported beside it (measured: split-bf16 kernels 4.6e-6 worst,
+    # the CPU fp32 oracle 1.7e-6).
+    ref64 = reference_grads(torch.float64)
+    params = reference_grads(torch.float32)
+    worst = worst_cpu = 0.0
+    for i, (gr, p, p64) in enumerate(zip(snap["grads"], params, ref64)):
+        e = rel_inf(gr, p64.grad)
         worst = max(worst, e)
-        assert e <= 5e-4, (i, e)
+        worst_cpu = max(worst_cpu, rel_inf(p.grad, p64.grad))
+        print(f"  grad {i}: GPU vs fp64 {e:.2e}, CPU fp32 vs fp64 {rel_inf(p.grad, p64.grad):.2e}, GPU vs CPU fp32 {rel_inf(gr, p.grad):.2e}")
+    assert worst <= 2e-5, (worst, worst_cpu)
+    del ref64
     norm = torch.nn.utils.clip_grad_norm_(params, 2.0, error_if_nonfinite=True)
     np.testing.assert_allclose(out["grad_norm"].item(), norm.item(), rtol=1e-4)
     torch.optim.Adam(params, lr=2e-4, betas=[0.9, 0.999], eps=1e-5).step()
     for i, (gp, p) in enumerate(zip(tr.params, params)):
         diff = np.abs(gp.detach().cpu().numpy() - p.detach().numpy())
         assert np.mean(diff > 2e-6) <= 5e-3 and diff.max() <= 4e-4, (i, np.mean(diff > 2e-6), diff.max())
-    print(f"512^2 step: worst per-tensor gradient rel_inf {worst:.2e}")
+    print(f"512^2 step: worst per-tensor gradient rel_inf vs float64 {worst:.2e} (CPU fp32 oracle: {worst_cpu:.2e})")
