@@ -86,6 +86,34 @@ def adain_train_shapes(batch=16, size=512):
     return seen
 
 
+def ast_shapes(batch=8, size=160):
+    """The conv3x3 launches of one ASTTrainer step (bench.py --mode ast-train: the loss network's
+    passes over the packed small planes and their input-gradient convs, the image convs)."""
+    from arbitrarystyletransfer_amd import models
+    from arbitrarystyletransfer_amd.train import ASTTrainer, default_ast_args
+    seen = []
+    orig = ops.conv3x3
+
+    def spy(x, w_packed, bias, cout, *, upsample=1, pad_mode="zeros", want_pool=False, x2=None, **kw):
+        n = int(x.shape[0]) + (int(x2.shape[0]) if x2 is not None else 0)
+        shp = (n, int(x.shape[1]), int(x.shape[2]), int(x.shape[3]), cout, upsample, pad_mode, want_pool)
+        if shp not in seen:
+            seen.append(shp)
+        return orig(x, w_packed, bias, cout, upsample=upsample, pad_mode=pad_mode, want_pool=want_pool, x2=x2, **kw)
+
+    ops.conv3x3 = spy
+    try:
+        tr = ASTTrainer(default_ast_args(batch_size=batch), device="cuda",
+                        ast=models.AST(attention=True).load_live_init(), graph=False)
+        c = torch.from_numpy(synth.image(905, (batch, 3, size, size))).cuda()
+        s = torch.from_numpy(synth.image(925, (batch, 3, size, size))).cuda()
+        tr.train_step(c, s, record=False)
+        torch.cuda.synchronize()
+    finally:
+        ops.conv3x3 = orig
+    return seen
+
+
 def key(n, cin, h, w, cout, up, pad, pool):
     return f"{n}x{cin}x{h}x{w}->{cout} up{up} {pad}{' pool' if pool else ''}"
 
@@ -121,7 +149,7 @@ def main():
         table = json.load(open(path))
     report = []
     todo = ae_shapes() if os.environ.get("TUNE_AE") else adain_train_shapes() if os.environ.get("TUNE_TRAIN") \
-        else shapes(batch)
+        else ast_shapes() if os.environ.get("TUNE_AST") else shapes(batch)
     if os.environ.get("TUNE_NEW"):  # only shapes the table does not hold yet
         todo = [t for t in todo if key(*t) not in table]
     if os.environ.get("TUNE_SMALL"):  # only the shapes the direct VALU kernels serve (cin or cout <= 4)
