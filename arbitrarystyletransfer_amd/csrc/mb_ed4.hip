@@ -69,6 +69,10 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 #ifndef ED4_TH
 #define ED4_TH 31  // output rows per band (TH + K - 1 a multiple of K for K = 3, 5)
 #endif
+#ifndef ED4_DOT2
+#define ED4_DOT2 0  // k5 stride-1 depthwise taps 0-3 on bf16 v_dot2 (A/B builds)
+#endif
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
 
 // WG4 (wo % 8 == 0): a workgroup is 4 waves on 4 adjacent strips (same channel block and band). Their
 // 4 x 28 output columns are contiguous, so each output row goes through one shared LDS image and
@@ -111,6 +115,18 @@ __global__ __launch_bounds__(WG4 ? 64 * ED4_WGN : 64, (K == 5 && KS >= 6) ? 1 : 
 #pragma unroll
   for (int i = 0; i < K * K; ++i) wk[i] = chv ? a.wdw[ch * K * K + i] : 0.f;
   const float bd = chv ? a.bdw[ch] : 0.f, b1 = (chv && !R1) ? a.b1[ch] : 0.f;
+#if ED4_DOT2
+  constexpr bool DOT2 = K == 5 && !R1;
+  bf2 wp[DOT2 ? K : 1][3];  // taps (0, 1), (2, 3), (4, 0) of each kernel row as bf16 pairs
+  if constexpr (DOT2) {
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      wp[ky][0] = bf2{(bf16)wk[ky * K], (bf16)wk[ky * K + 1]};
+      wp[ky][1] = bf2{(bf16)wk[ky * K + 2], (bf16)wk[ky * K + 3]};
+      wp[ky][2] = bf2{(bf16)wk[ky * K + 4], (bf16)0.f};
+    }
+  }
+#endif
   const int hid16 = (a.hid + 15) / 16 * 16;
   bf16x8 bw[KS];  // B[k = 8h + j][col r] = W1[ch][16 s + 8h + j]; R1: identity on the block's channels
 #pragma unroll
@@ -272,18 +288,39 @@ __global__ __launch_bounds__(WG4 ? 64 * ED4_WGN : 64, (K == 5 && KS >= 6) ? 1 : 
       e[1] = r1;
       e[18] = r0;  // half 0: columns 16, 17 (likewise unused by half 1)
       e[19] = r1;
+#if ED4_DOT2
+      // k5 taps as bf16 pairs on v_dot2c_f32_bf16 (fp32 accumulate): (0, 1), (2, 3), (4, zero)
+      bf2 E[DOT2 ? 20 : 1];
+      if constexpr (DOT2) {
+#pragma unroll
+        for (int m = 0; m < 20; ++m) E[m] = bf2{(bf16)e[m], m + 1 < 20 ? (bf16)e[m + 1] : (bf16)0.f};
+      }
+#endif
 #pragma unroll
       for (int ky = K - 1; ky >= 0; --ky) {
         const int orow = j - ky;
         const int slot = ((u - ky) % K + K) % K;
         const bool live = orow >= 0 && orow < TH;  // uniform
         if (live) {
+#if ED4_DOT2
+          if constexpr (DOT2) {
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            float v = ky == 0 ? bd : acc[slot][i];
+            for (int i = 0; i < 16; ++i) {
+              float v = ky == 0 ? bd : acc[slot][i];
+              v = __builtin_amdgcn_fdot2_f32_bf16(wp[ky][0], E[i], v, false);
+              v = __builtin_amdgcn_fdot2_f32_bf16(wp[ky][1], E[i + 2], v, false);
+              acc[slot][i] = __builtin_amdgcn_fdot2_f32_bf16(wp[ky][2], E[i + 4], v, false);
+            }
+          } else
+#endif
+          {
 #pragma unroll
-            for (int kx = 0; kx < K; ++kx) v = fmaf(wk[ky * K + kx], e[i + 2 - P + kx], v);
-            acc[slot][i] = v;
+            for (int i = 0; i < 16; ++i) {
+              float v = ky == 0 ? bd : acc[slot][i];
+#pragma unroll
+              for (int kx = 0; kx < K; ++kx) v = fmaf(wk[ky * K + kx], e[i + 2 - P + kx], v);
+              acc[slot][i] = v;
+            }
           }
         }
         if (ky == K - 1) finish(orow, acc[slot], live);
