@@ -147,6 +147,131 @@ __global__ void pad_up_adjoint_full_kernel(const float* __restrict__ dp, float* 
   }
 }
 
+// Row-parallel forms of the three kernels above (the defaults where the row width allows): a thread
+// owns 4 consecutive columns of one (plane, row) with 16-byte loads/stores where aligned, and the
+// index math is one 32-bit division per 4 outputs -- the flat forms spent their time in 64-bit
+// div/mod per element (config 3: ~10 ms per step over 32 launches, HBM-bound work of ~5).
+__global__ __launch_bounds__(256) void act_backward_v4_kernel(const float* __restrict__ pre,
+                                                              const float* __restrict__ g_pre,
+                                                              const float* __restrict__ g_act,
+                                                              const float* __restrict__ g_pool,
+                                                              float* __restrict__ dy, unsigned nq, int H, int W) {
+  const unsigned q = (unsigned)W >> 2;  // quads per row (W % 4 == 0)
+  const int Ho = H >> 1, Wo = W >> 1;
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < nq; t += gridDim.x * blockDim.x) {
+    const unsigned row = t / q, x0 = 4 * (t - row * q);
+    const unsigned p = row / (unsigned)H;
+    const int y = (int)(row - p * (unsigned)H);
+    const int64_t off = (int64_t)row * W + x0;
+    const float4 v4 = *reinterpret_cast<const float4*>(pre + off);
+    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+    float g[4] = {0.f, 0.f, 0.f, 0.f}, a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (g_pre) {
+      const float4 u = *reinterpret_cast<const float4*>(g_pre + off);
+      g[0] = u.x; g[1] = u.y; g[2] = u.z; g[3] = u.w;
+    }
+    if (g_act) {
+      const float4 u = *reinterpret_cast<const float4*>(g_act + off);
+      a[0] = u.x; a[1] = u.y; a[2] = u.z; a[3] = u.w;
+    }
+    const int py = y >> 1;
+    if (g_pool && py < Ho) {
+      // the 2x2 windows (py, x0/2) and (py, x0/2 + 1): this row and its partner row
+      const int64_t top = ((int64_t)p * H + 2 * py) * W + x0;
+      const float4 r0 = *reinterpret_cast<const float4*>(pre + top);
+      const float4 r1 = *reinterpret_cast<const float4*>(pre + top + W);
+      const float c0[4] = {r0.x, r0.y, r0.z, r0.w}, c1[4] = {r1.x, r1.y, r1.z, r1.w};
+      const float2 gp = *reinterpret_cast<const float2*>(g_pool + ((int64_t)p * Ho + py) * Wo + (x0 >> 1));
+      const float gpw[2] = {gp.x, gp.y};
+#pragma unroll
+      for (int w2 = 0; w2 < 2; ++w2) {
+        const int px = (int)(x0 >> 1) + w2;
+        if (px >= Wo) continue;
+        const float c[4] = {relu_f(c0[2 * w2]), relu_f(c0[2 * w2 + 1]), relu_f(c1[2 * w2]), relu_f(c1[2 * w2 + 1])};
+        int best = 0;
+#pragma unroll
+        for (int qq = 1; qq < 4; ++qq)
+          if (c[qq] > c[best] || c[qq] != c[qq]) best = qq;  // torch: val > max || isnan(val)
+        if ((best >> 1) == (y & 1)) a[2 * w2 + (best & 1)] += gpw[w2];
+      }
+    }
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = v[j] > 0.f ? g[j] + a[j] : g[j];
+    *reinterpret_cast<float4*>(dy + off) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+__global__ __launch_bounds__(256) void pad_grad_v4_kernel(const float* __restrict__ g, const float* __restrict__ mask,
+                                                          float* __restrict__ out, unsigned nq, int H, int W, int Wp) {
+  const unsigned q = (unsigned)Wp >> 2;  // Wp % 4 == 0
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < nq; t += gridDim.x * blockDim.x) {
+    const unsigned orow = t / q;
+    const int c0 = 4 * (int)(t - orow * q);
+    const unsigned p = orow / (unsigned)(H + 2);
+    const int r = (int)(orow - p * (unsigned)(H + 2));
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r >= 1 && r <= H) {
+      const int64_t srow = ((int64_t)p * H + (r - 1)) * W;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + j;
+        if (c >= 1 && c <= W) {
+          float v = g[srow + c - 1];
+          if (mask && !(mask[srow + c - 1] > 0.f)) v = 0.f;
+          o[j] = v;
+        }
+      }
+    }
+    *reinterpret_cast<float4*>(out + (int64_t)orow * Wp + c0) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// (same sums and summation order as pad_up_adjoint_full_kernel)
+template <int UP>
+__global__ __launch_bounds__(256) void pad_up_adjoint_v4_kernel(const float* __restrict__ dp, float* __restrict__ dx,
+                                                                unsigned nq, int h_in, int w_in, int Wp) {
+  const int H = h_in * UP, W = w_in * UP;
+  const unsigned q = (unsigned)w_in >> 2;  // w_in % 4 == 0
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < nq; t += gridDim.x * blockDim.x) {
+    const unsigned row = t / q;
+    const int vx0 = 4 * (int)(t - row * q);
+    const unsigned p = row / (unsigned)h_in;
+    const int vy = (int)(row - p * (unsigned)h_in);
+    int rows[4], nr = 0;
+#pragma unroll
+    for (int k = 0; k < UP; ++k) rows[nr++] = UP * vy + k + 1;
+    if (UP == 1) {
+      if (vy == 1) rows[nr++] = 0;
+      if (vy == H - 2) rows[nr++] = H + 1;
+    } else {
+      if (vy == 0) rows[nr++] = 0;
+      if (vy == h_in - 1) rows[nr++] = H + 1;
+    }
+    const float* d = dp + (int64_t)p * (H + 2) * Wp;
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int vx = vx0 + j;
+      int cols[4], nc = 0;
+#pragma unroll
+      for (int k = 0; k < UP; ++k) cols[nc++] = UP * vx + k + 1;
+      if (UP == 1) {
+        if (vx == 1) cols[nc++] = 0;
+        if (vx == W - 2) cols[nc++] = W + 1;
+      } else {
+        if (vx == 0) cols[nc++] = 0;
+        if (vx == w_in - 1) cols[nc++] = W + 1;
+      }
+      float s = 0.f;
+      for (int a = 0; a < nr; ++a)
+        for (int b = 0; b < nc; ++b) s += d[(int64_t)rows[a] * Wp + cols[b]];
+      o[j] = s;
+    }
+    *reinterpret_cast<float4*>(dx + (int64_t)row * w_in + vx0) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // dx = g * (mask > 0) (ReLU backward given the ReLU output).
 __global__ void relu_mask_kernel(const float* __restrict__ g, const float* __restrict__ mask, float* __restrict__ out,
                                  int64_t n) {
@@ -776,6 +901,11 @@ __global__ __launch_bounds__(256, 2) void wgrad3_kernel(WgArgs a) {
 }
 
 int g_wgrad_v1 = 0;  // AST_WGRAD_V1=1: always the general kernel (A/B measurements)
+// AST_BWD_ROWPAR=0: the flat elementwise backward kernels (A/B measurements)
+const int g_rowpar = [] {
+  const char* v = getenv("AST_BWD_ROWPAR");
+  return v ? atoi(v) : 1;
+}();
 
 int grid1(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
@@ -805,6 +935,14 @@ int ast_conv_act_backward_f32(const float* pre, const float* g_pre, const float*
                               float* dy, long long planes, int h, int w, void* stream) {
   if (!pre || !dy) return AST_E_NULLPTR;
   if (planes <= 0 || h <= 0 || w <= 0) return AST_E_SHAPE;
+  const bool al = ((((uintptr_t)pre | (uintptr_t)g_pre | (uintptr_t)g_act | (uintptr_t)dy) & 15) == 0) &&
+                  (((uintptr_t)g_pool & 7) == 0);
+  if (g_rowpar && w % 4 == 0 && al && planes * h * (w / 4) < 0x7fffffffLL) {
+    const unsigned nq = (unsigned)(planes * h * (w / 4));
+    hipLaunchKernelGGL(act_backward_v4_kernel, dim3(grid1(nq)), dim3(256), 0, (hipStream_t)stream, pre, g_pre, g_act,
+                       g_pool, dy, nq, h, w);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(act_backward_kernel, dim3(grid1(planes * h * w)), dim3(256), 0, (hipStream_t)stream, pre, g_pre,
                      g_act, g_pool, dy, (int64_t)planes, h, w);
   return (int)hipGetLastError();
@@ -821,6 +959,12 @@ int ast_grad_pad_f32(const float* g, const float* mask, float* out_pad, long lon
                      void* stream) {
   if (!g || !out_pad) return AST_E_NULLPTR;
   if (planes <= 0 || h <= 0 || w <= 0 || pitch < w + 2) return AST_E_SHAPE;
+  if (g_rowpar && pitch % 4 == 0 && ((uintptr_t)out_pad & 15) == 0 && planes * (h + 2) * (pitch / 4) < 0x7fffffffLL) {
+    const unsigned nq = (unsigned)(planes * (h + 2) * (pitch / 4));
+    hipLaunchKernelGGL(pad_grad_v4_kernel, dim3(grid1(nq)), dim3(256), 0, (hipStream_t)stream, g, mask, out_pad, nq, h,
+                       w, pitch);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(pad_grad_kernel, dim3(grid1(planes * (h + 2) * pitch)), dim3(256), 0, (hipStream_t)stream, g,
                      mask, out_pad, (int64_t)planes, h, w, pitch);
   return (int)hipGetLastError();
@@ -832,6 +976,16 @@ int ast_pad_up_adjoint_f32(const float* dp_full, float* dx, long long planes, in
   if (planes <= 0 || h_in <= 0 || w_in <= 0) return AST_E_SHAPE;
   if (upsample != 1 && upsample != 2) return AST_E_UNSUPPORTED;
   if (h_in * upsample < 2 || w_in * upsample < 2 || pitch < w_in * upsample + 2) return AST_E_SHAPE;
+  if (g_rowpar && w_in % 4 == 0 && ((uintptr_t)dx & 15) == 0 && planes * h_in * (w_in / 4) < 0x7fffffffLL) {
+    const unsigned nq = (unsigned)(planes * h_in * (w_in / 4));
+    if (upsample == 1)
+      hipLaunchKernelGGL(pad_up_adjoint_v4_kernel<1>, dim3(grid1(nq)), dim3(256), 0, (hipStream_t)stream, dp_full, dx,
+                         nq, h_in, w_in, pitch);
+    else
+      hipLaunchKernelGGL(pad_up_adjoint_v4_kernel<2>, dim3(grid1(nq)), dim3(256), 0, (hipStream_t)stream, dp_full, dx,
+                         nq, h_in, w_in, pitch);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(pad_up_adjoint_full_kernel, dim3(grid1(planes * h_in * w_in)), dim3(256), 0, (hipStream_t)stream,
                      dp_full, dx, (int64_t)planes, h_in, w_in, upsample, pitch);
   return (int)hipGetLastError();

@@ -318,6 +318,9 @@ __global__ void tv_kernel(const float* __restrict__ x, int64_t planes, int H, in
 // Gram forward: G[blockIdx.y][b][i][j] = s * sum_{k in split} F[b][i][k] F[b][j][k], k-range split over
 // blockIdx.y (G is the gram itself with one split, else the workspace of partial tiles).
 // 64x64 output tile, 4 waves (2x2 of 32x32), BK = 32; F tiles transposed into LDS [k][row].
+// G is symmetric: only the tiles ti <= tj are computed (blockIdx.x enumerates
+// them row by row), an off-diagonal tile is stored at (ti, tj) and mirrored at (tj, ti), a diagonal
+// tile's upper half is stored and mirrored (G is exactly symmetric, whatever the summation order).
 // ------------------------------------------------------------------------------------------
 constexpr int GT = 64, GBK = 32;
 
@@ -326,7 +329,12 @@ __global__ __launch_bounds__(256) void gram_kernel(const float* __restrict__ F, 
   __shared__ float As[GBK][GT + 4];
   __shared__ float Bs[GBK][GT + 4];
   const int tiles = (C + GT - 1) / GT;
-  const int ti = blockIdx.x % tiles, tj = blockIdx.x / tiles;
+  int ti = 0, tj = blockIdx.x;  // upper-triangle index -> (ti, tj), ti <= tj
+  while (tj >= tiles - ti) {
+    tj -= tiles - ti;
+    ++ti;
+  }
+  tj += ti;
   const int b = blockIdx.z;
   const int64_t k0 = (int64_t)blockIdx.y * kchunk;
   const int64_t k1 = min(K, k0 + kchunk);
@@ -377,7 +385,10 @@ __global__ __launch_bounds__(256) void gram_kernel(const float* __restrict__ F, 
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int i = ti * GT + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (i < C && j < C) Gb[(int64_t)i * C + j] = s * acc[r];
+    if (i < C && j < C && (ti != tj || i <= j)) {  // diagonal tiles: the upper half, mirrored
+      Gb[(int64_t)i * C + j] = s * acc[r];
+      Gb[(int64_t)j * C + i] = s * acc[r];
+    }
   }
 }
 
@@ -507,7 +518,7 @@ int ast_gram_f32(const float* feat, float* gram, int n, int c, long long hw, flo
     if (!workspace) return AST_E_NULLPTR;
     if (workspace_floats < ast_gram_workspace_floats(n, c, hw)) return AST_E_SHAPE;
   }
-  hipLaunchKernelGGL(gram_kernel, dim3(tiles * tiles, (unsigned)splits, n), dim3(256), 0, s, feat,
+  hipLaunchKernelGGL(gram_kernel, dim3(tiles * (tiles + 1) / 2, (unsigned)splits, n), dim3(256), 0, s, feat,
                      splits > 1 ? workspace : gram, c, (int64_t)hw, kchunk, scale);
   if (splits > 1) {
     const int64_t cnt = (int64_t)n * c * c;

@@ -166,8 +166,8 @@ def test_loss_functions_golden(golden, hip_device):
 
 @pytest.mark.parametrize("shape", [(2, 192, 37, 41), (1, 512, 32, 32), (3, 64, 128, 128), (2, 5, 9, 7)])
 def test_gram_vs_oracle(shape, hip_device):
-    """gram_matrix (losses.py:105-109) on the split-bf16 kernel: the upper-triangle tiles, mirrored
-    (exactly symmetric), split-K partials summed in order; against float64 at the fp32 bar."""
+    """gram_matrix (losses.py:105-109): the upper-triangle tiles, mirrored (exactly symmetric),
+    split-K partials summed in order; against float64 at the fp32 bar."""
     x = rnd(31, shape, 1.0, 0.3)
     ref = R.gram_matrix(x.double())
     got = L.gram_matrix(x.to(hip_device))
