@@ -159,16 +159,42 @@ __global__ __launch_bounds__(kThreads) void mvn_huber_kernel(const float* __rest
 }
 
 // Backward: dx = c * (huber'(d) - mean(g) - z * sum(g z)/(N-1)) / sd_x, one read of x and y.
-__global__ void mvn_huber_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
-                                     const float* __restrict__ pstats, int64_t hw, int64_t n, float c,
-                                     const float* __restrict__ gscale, float* __restrict__ dx, int accumulate) {
+// grid (pixel chunks of 4 * kThreads, planes strided by gridDim.y): the plane's statistics are read
+// once, 16-byte accesses where the plane is 4-aligned, no per-element index division.
+__global__ __launch_bounds__(kThreads) void mvn_huber_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                                 const float* __restrict__ pstats, int64_t hw,
+                                                                 int64_t planes, float c,
+                                                                 const float* __restrict__ gscale, float* __restrict__ dx,
+                                                                 int accumulate) {
   const float cc = c * gs(gscale);
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
-    const float* s = pstats + 6 * (i / hw);
-    const float z = (x[i] - s[0]) / s[1];
-    const float d = z - (y[i] - s[2]) / s[3];
-    const float v = cc * (huber_grad(d) - s[4] - z * s[5]) / s[1];
-    dx[i] = accumulate ? dx[i] + v : v;
+  const bool vec = (hw & 3) == 0 && ((((uintptr_t)x | (uintptr_t)y | (uintptr_t)dx) & 15) == 0);
+  for (int64_t p = blockIdx.y; p < planes; p += gridDim.y) {
+    const float* s = pstats + 6 * p;
+    const float s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3], s4 = s[4], s5 = s[5];
+    const float* xp = x + p * hw;
+    const float* yp = y + p * hw;
+    float* dp = dx + p * hw;
+    auto one = [&](float xv, float yv) {
+      const float z = (xv - s0) / s1;
+      const float d = z - (yv - s2) / s3;
+      return cc * (huber_grad(d) - s4 - z * s5) / s1;
+    };
+    for (int64_t i = ((int64_t)blockIdx.x * kThreads + threadIdx.x) * 4; i < hw; i += (int64_t)gridDim.x * kThreads * 4) {
+      if (vec) {
+        const float4 xv = *reinterpret_cast<const float4*>(xp + i), yv = *reinterpret_cast<const float4*>(yp + i);
+        float4 v = make_float4(one(xv.x, yv.x), one(xv.y, yv.y), one(xv.z, yv.z), one(xv.w, yv.w));
+        if (accumulate) {
+          const float4 o = *reinterpret_cast<const float4*>(dp + i);
+          v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+        }
+        *reinterpret_cast<float4*>(dp + i) = v;
+      } else {
+        for (int64_t j = i; j < i + 4 && j < hw; ++j) {
+          const float v = one(xp[j], yp[j]);
+          dp[j] = accumulate ? dp[j] + v : v;
+        }
+      }
+    }
   }
 }
 
@@ -555,10 +581,11 @@ int ast_mvn_huber_backward_f32(const float* x, const float* y, const float* psta
                                float weight, const float* gscale, float* dx, int accumulate, void* stream) {
   if (!x || !y || !pstats || !dx) return AST_E_NULLPTR;
   if (planes <= 0 || hw <= 1) return AST_E_SHAPE;
-  const int64_t n = (int64_t)planes * hw;
-  hipLaunchKernelGGL(mvn_huber_bwd_kernel, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, x, y, pstats,
-                     (int64_t)hw, n, (float)((double)weight / ((double)planes * hw)), gscale, dx,
-                     accumulate ? 1 : 0);
+  const int64_t chunks = std::min<int64_t>((hw + 4 * kThreads - 1) / (4 * kThreads), 4096);
+  const int64_t py = std::max<int64_t>(1, std::min<int64_t>(planes, 65535));
+  hipLaunchKernelGGL(mvn_huber_bwd_kernel, dim3((unsigned)chunks, (unsigned)py), dim3(kThreads), 0, (hipStream_t)stream,
+                     x, y, pstats, (int64_t)hw, (int64_t)planes, (float)((double)weight / ((double)planes * hw)), gscale,
+                     dx, accumulate ? 1 : 0);
   return (int)hipGetLastError();
 }
 
