@@ -202,35 +202,52 @@ __global__ __launch_bounds__(256) void act_backward_v4_kernel(const float* __res
   }
 }
 
+// out[r][c] = g[r-1][c-1]: output quad q holds input columns 4q-1 .. 4q+2 = (quad q-1).w, (quad
+// q).xyz -- two aligned 16-byte loads (the neighbour thread's quad comes from L1/L2), W % 4 == 0
 __global__ __launch_bounds__(256) void pad_grad_v4_kernel(const float* __restrict__ g, const float* __restrict__ mask,
                                                           float* __restrict__ out, unsigned nq, int H, int W, int Wp) {
   const unsigned q = (unsigned)Wp >> 2;  // Wp % 4 == 0
+  const int wq = W >> 2;                 // input quads per row
   for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < nq; t += gridDim.x * blockDim.x) {
     const unsigned orow = t / q;
-    const int c0 = 4 * (int)(t - orow * q);
+    const int oq = (int)(t - orow * q), c0 = 4 * oq;
     const unsigned p = orow / (unsigned)(H + 2);
     const int r = (int)(orow - p * (unsigned)(H + 2));
     float o[4] = {0.f, 0.f, 0.f, 0.f};
     if (r >= 1 && r <= H) {
-      const int64_t srow = ((int64_t)p * H + (r - 1)) * W;
+      const float* grow = g + ((int64_t)p * H + (r - 1)) * W;
+      const float* mrow = mask ? mask + ((int64_t)p * H + (r - 1)) * W : nullptr;
+      float in[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // input columns c0 - 4 + 3 .. c0 + 3: in[j] = column c0 - 1 + j
+      float mk[5] = {1.f, 1.f, 1.f, 1.f, 1.f};
+      if (oq >= 1 && oq - 1 < wq) {
+        in[0] = grow[c0 - 1];
+        if (mrow) mk[0] = mrow[c0 - 1];
+      }
+      if (oq < wq) {
+        const float4 v = *reinterpret_cast<const float4*>(grow + c0);
+        in[1] = v.x; in[2] = v.y; in[3] = v.z; in[4] = v.w;
+        if (mrow) {
+          const float4 m = *reinterpret_cast<const float4*>(mrow + c0);
+          mk[1] = m.x; mk[2] = m.y; mk[3] = m.z; mk[4] = m.w;
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c = c0 + j;
-        if (c >= 1 && c <= W) {
-          float v = g[srow + c - 1];
-          if (mask && !(mask[srow + c - 1] > 0.f)) v = 0.f;
-          o[j] = v;
-        }
+        if (c >= 1 && c <= W) o[j] = (mrow && !(mk[j] > 0.f)) ? 0.f : in[j];
       }
     }
     *reinterpret_cast<float4*>(out + (int64_t)orow * Wp + c0) = make_float4(o[0], o[1], o[2], o[3]);
   }
 }
 
-// (same sums and summation order as pad_up_adjoint_full_kernel)
+// (same sums and summation order as pad_up_adjoint_full_kernel). A row's main columns come from
+// aligned 16-byte loads: UP = 1, columns vx0 + 1 .. vx0 + 4 from the two quads at vx0; UP = 2,
+// columns 2 vx0 + 1 .. 2 vx0 + 8 from the three quads at 2 vx0 (host: Wp % 4 == 0, Wp >= W + 4).
 template <int UP>
 __global__ __launch_bounds__(256) void pad_up_adjoint_v4_kernel(const float* __restrict__ dp, float* __restrict__ dx,
                                                                 unsigned nq, int h_in, int w_in, int Wp) {
+  constexpr int NW = UP == 1 ? 8 : 12;  // window of loaded columns
   const int H = h_in * UP, W = w_in * UP;
   const unsigned q = (unsigned)w_in >> 2;  // w_in % 4 == 0
   for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < nq; t += gridDim.x * blockDim.x) {
@@ -249,26 +266,32 @@ __global__ __launch_bounds__(256) void pad_up_adjoint_v4_kernel(const float* __r
       if (vy == h_in - 1) rows[nr++] = H + 1;
     }
     const float* d = dp + (int64_t)p * (H + 2) * Wp;
-    float o[4];
+    const int cb = UP * vx0;  // first loaded column
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < nr; ++a) {
+      const float* dr = d + (int64_t)rows[a] * Wp;
+      float win[NW];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int vx = vx0 + j;
-      int cols[4], nc = 0;
-#pragma unroll
-      for (int k = 0; k < UP; ++k) cols[nc++] = UP * vx + k + 1;
-      if (UP == 1) {
-        if (vx == 1) cols[nc++] = 0;
-        if (vx == W - 2) cols[nc++] = W + 1;
-      } else {
-        if (vx == 0) cols[nc++] = 0;
-        if (vx == w_in - 1) cols[nc++] = W + 1;
+      for (int k = 0; k < NW / 4; ++k) {
+        const float4 v = *reinterpret_cast<const float4*>(dr + cb + 4 * k);
+        win[4 * k] = v.x; win[4 * k + 1] = v.y; win[4 * k + 2] = v.z; win[4 * k + 3] = v.w;
       }
-      float s = 0.f;
-      for (int a = 0; a < nr; ++a)
-        for (int b = 0; b < nc; ++b) s += d[(int64_t)rows[a] * Wp + cols[b]];
-      o[j] = s;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int vx = vx0 + j;
+        // the columns of pad_up_adjoint_full_kernel, in its order
+#pragma unroll
+        for (int k = 0; k < UP; ++k) s[j] += win[UP * j + k + 1];
+        if (UP == 1) {
+          if (vx == 1) s[j] += dr[0];
+          if (vx == W - 2) s[j] += dr[W + 1];
+        } else {
+          if (vx == 0) s[j] += dr[0];
+          if (vx == w_in - 1) s[j] += dr[W + 1];
+        }
+      }
     }
-    *reinterpret_cast<float4*>(dx + (int64_t)row * w_in + vx0) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(dx + (int64_t)row * w_in + vx0) = make_float4(s[0], s[1], s[2], s[3]);
   }
 }
 
@@ -959,7 +982,8 @@ int ast_grad_pad_f32(const float* g, const float* mask, float* out_pad, long lon
                      void* stream) {
   if (!g || !out_pad) return AST_E_NULLPTR;
   if (planes <= 0 || h <= 0 || w <= 0 || pitch < w + 2) return AST_E_SHAPE;
-  if (g_rowpar && pitch % 4 == 0 && ((uintptr_t)out_pad & 15) == 0 && planes * (h + 2) * (pitch / 4) < 0x7fffffffLL) {
+  if (g_rowpar && pitch % 4 == 0 && w % 4 == 0 && ((((uintptr_t)out_pad | (uintptr_t)g | (uintptr_t)mask) & 15) == 0) &&
+      planes * (h + 2) * (pitch / 4) < 0x7fffffffLL) {
     const unsigned nq = (unsigned)(planes * (h + 2) * (pitch / 4));
     hipLaunchKernelGGL(pad_grad_v4_kernel, dim3(grid1(nq)), dim3(256), 0, (hipStream_t)stream, g, mask, out_pad, nq, h,
                        w, pitch);
@@ -976,7 +1000,8 @@ int ast_pad_up_adjoint_f32(const float* dp_full, float* dx, long long planes, in
   if (planes <= 0 || h_in <= 0 || w_in <= 0) return AST_E_SHAPE;
   if (upsample != 1 && upsample != 2) return AST_E_UNSUPPORTED;
   if (h_in * upsample < 2 || w_in * upsample < 2 || pitch < w_in * upsample + 2) return AST_E_SHAPE;
-  if (g_rowpar && w_in % 4 == 0 && ((uintptr_t)dx & 15) == 0 && planes * h_in * (w_in / 4) < 0x7fffffffLL) {
+  if (g_rowpar && w_in % 4 == 0 && pitch % 4 == 0 && pitch >= w_in * upsample + 4 &&
+      ((((uintptr_t)dx | (uintptr_t)dp_full) & 15) == 0) && planes * h_in * (w_in / 4) < 0x7fffffffLL) {
     const unsigned nq = (unsigned)(planes * h_in * (w_in / 4));
     if (upsample == 1)
       hipLaunchKernelGGL(pad_up_adjoint_v4_kernel<1>, dim3(grid1(nq)), dim3(256), 0, (hipStream_t)stream, dp_full, dx,
