@@ -176,6 +176,92 @@ __global__ __launch_bounds__(kT) void gemm_kernel(GemmArgs a) {
   }
 }
 
+// Wide-N form for the forward / input-gradient 1x1 convs (batch 1, B and C pixel-contiguous, no K
+// split, pixels per image a multiple of 4): 64 (m) x 256 (n) per workgroup, so each B row is read
+// as one 1 KB run per wave instruction (16-byte loads) -- gemm_kernel's 64-column tiles read
+// 256-byte runs of 16-240 rows that lie 100 KB apart and streamed at 2.3-2.7 TB/s
+// (profiles/r03_gemm_probe.txt). Wave w owns columns 64w .. 64w + 63 and all 64 rows (2 x 2
+// accumulators of 32 x 32; the second row block is skipped when M <= 32); K in chunks of 16 with
+// the next chunk's loads in flight during the MFMAs. Same products and k order as gemm_kernel.
+constexpr int WGN = 256, WGK = 16;
+
+__global__ __launch_bounds__(kT) void gemm_wide_kernel(GemmArgs a, int P) {
+  __shared__ float As[WGK][GT + 4];   // [k][m]
+  __shared__ float Bs[WGK][WGN + 4];  // [k][n]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.y * GT;
+  const int n0 = blockIdx.x * WGN;
+  const bool two = m0 + 32 < a.M;  // second 32-row block live (uniform)
+  // B staging: quad qn = tid & 63 of row kr = (tid >> 6) + 4 i; A staging: row m = tid >> 2, k 4 (tid & 3) + j
+  const int qn = tid & 63, kr0 = tid >> 6;
+  const int nq = n0 + 4 * qn;
+  const bool nv = nq < a.N;  // a quad never straddles images (P % 4 == 0, N % 4 == 0)
+  const int img = nv ? nq / P : 0;
+  const float* bbase = a.B + (int64_t)img * a.sBb + (nq - img * P);
+  const int am = tid >> 2, ak = 4 * (tid & 3);
+  const bool amv = m0 + am < a.M;
+  const float* abase = a.A + (int64_t)(m0 + am) * a.sAm;
+  float4 rb[4];
+  float ra[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = k0 + kr0 + 4 * i;
+      rb[i] = (nv && k < a.K) ? *reinterpret_cast<const float4*>(bbase + (int64_t)k * a.sBk) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + ak + j;
+      ra[j] = (amv && k < a.K) ? abase[(int64_t)k * a.sAk] : 0.f;
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0.f};
+  load(0);
+  for (int k0 = 0; k0 < a.K; k0 += WGK) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(&Bs[kr0 + 4 * i][4 * qn]) = rb[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) As[ak + j][am] = ra[j];
+    __syncthreads();
+    if (k0 + WGK < a.K) load(k0 + WGK);
+#pragma unroll
+    for (int kp = 0; kp < WGK / 2; ++kp) {
+      const float a0 = As[2 * kp + h][r], a1 = As[2 * kp + h][32 + r];
+      const float b0 = Bs[2 * kp + h][64 * wave + r], b1 = Bs[2 * kp + h][64 * wave + 32 + r];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      if (two) {
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int n = n0 + 64 * wave + 32 * ni + r;
+    if (n >= a.N) continue;
+    const int im = n / P;
+    float* cc = a.C + (int64_t)im * a.sCb + (n - im * P);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      if (mi == 1 && !two) break;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = m0 + 32 * mi + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (m < a.M) {
+          float* c = cc + (int64_t)m * a.sCm;
+          *c = a.accumulate ? *c + acc[mi][ni][i] : acc[mi][ni][i];
+        }
+      }
+    }
+  }
+}
+
 // C[b][m][n] (+)= sum over the tiles z of C's image (z = b * ksplit + ks; all z when C is shared
 // across the batch, sCb == 0) of part[z][m][n], in z order.
 __global__ __launch_bounds__(kT) void gemm_reduce_kernel(GemmArgs a, int zper) {
@@ -915,6 +1001,19 @@ int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int
     return v ? atoi(v) : 0;
   }();
   const dim3 grid((unsigned)((N + GT - 1) / GT), (unsigned)((M + GT - 1) / GT), (unsigned)(batch * ksplit));
+  static const int wide = [] {  // AST_MBGEMM_WIDE=0: gemm_kernel for these shapes too (A/B measurements)
+    const char* v = getenv("AST_MBGEMM_WIDE");
+    return v ? atoi(v) : 1;
+  }();
+  {
+    const int P = foldN ? foldN : N;
+    if (wide && !x3 && batch == 1 && ksplit == 1 && !foldK && sBn == 1 && sCn == 1 && need == 0 && P % 4 == 0 &&
+        N % 4 == 0 && sBk % 4 == 0 && (foldN == 0 || sBb % 4 == 0) && ((uintptr_t)B & 15) == 0) {
+      const dim3 g((unsigned)((N + WGN - 1) / WGN), (unsigned)((M + GT - 1) / GT));
+      hipLaunchKernelGGL(gemm_wide_kernel, g, dim3(kT), 0, st, a, P);
+      return (int)hipGetLastError();
+    }
+  }
   if (x3 && (foldK == 0 || foldK % 8 == 0)) {  // split-bf16 path (8 consecutive k stay in one image)
     auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     X3Flags fl{};
