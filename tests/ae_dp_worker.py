@@ -30,6 +30,11 @@ def main(out_path):
         orig()
 
     tr.ae_optim.step = step
+    poison = os.environ.get("AST_POISON")
+    if poison:   # debugging aid: fill the caching allocator's free blocks so unwritten reads show
+        big = [torch.full((1 << 28,), float(poison), device="cuda:0") for _ in range(4)]
+        small = [torch.full((1 << 18,), float(poison), device="cuda:0") for _ in range(256)]
+        del big, small
     out = tr.train_step(content[a:b].cuda())
     losses = torch.stack([out[k].detach().float() for k in ("recon_loss", "content_loss", "loss")]).cpu()
     dist.all_reduce(losses)
