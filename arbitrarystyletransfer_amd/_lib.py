@@ -47,6 +47,9 @@ SIGNATURES = {
     "ast_gram_f32": (_i, [_p, _p, _i, _i, _ll, _f, _p, _ll, _p]),
     "ast_gram_backward_f32": (_i, [_p, _p, _p, _p, _p, _i, _i, _ll, _f, _p, _i, _p]),
     "ast_mvn_huber_f32": (_i, [_p, _p, _ll, _ll, _f, _p, _p, _p]),
+    "ast_plane_stats_workspace_floats": (_ll, [_ll, _ll]),
+    "ast_mvn_huber_ws_f32": (_i, [_p, _p, _ll, _ll, _f, _p, _p, _p, _ll, _p]),
+    "ast_style_moments_ws_f32": (_i, [_p, _p, _ll, _ll, _f, _p, _p, _p, _p, _p, _p, _ll, _p]),
     "ast_mvn_huber_backward_f32": (_i, [_p, _p, _p, _ll, _ll, _f, _p, _p, _i, _p]),
     "ast_huber_f32": (_i, [_p, _p, _ll, _f, _p, _p, _p, _i, _p]),
     "ast_style_moments_f32": (_i, [_p, _p, _ll, _ll, _f, _p, _p, _p, _p, _p, _p]),

@@ -198,6 +198,182 @@ __global__ __launch_bounds__(kThreads) void mvn_huber_bwd_kernel(const float* __
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Split-plane forms (the *_ws entries): a plane is cut into chunks of kChunk elements, one
+// workgroup per (chunk, plane), 16-byte loads where the planes are 4-aligned. The one-workgroup-
+// per-plane kernels above leave most of the chip idle on few, large planes (48 image planes of
+// 512^2: 0.86 ms for 200 MB) and read with 4-byte loads. Partials go to the workspace and are
+// merged in chunk order (det.h), so results do not depend on workgroup timing.
+//   part  [planes][nchunks][6]: (count, mean_x, M2_x, mean_y, M2_y, -) of the chunk
+//   hpart [planes][nchunks][4]: (sum huber, sum g, sum g z, -) of the chunk
+// ------------------------------------------------------------------------------------------
+constexpr int kChunk = 8192;
+
+__device__ __forceinline__ bool vec4_ok(const float* x, const float* y, int64_t hw) {
+  return (hw & 3) == 0 && ((((uintptr_t)x | (uintptr_t)y) & 15) == 0);
+}
+
+__global__ __launch_bounds__(kThreads) void moments_part_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                                int64_t planes, int64_t hw, int nchunks,
+                                                                float* __restrict__ part) {
+  __shared__ float sh[12];
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk, c1 = min(hw, c0 + (int64_t)kChunk);
+  const bool vec = vec4_ok(x, y, hw);
+  for (int64_t p = blockIdx.y; p < planes; p += gridDim.y) {
+    const float* xp = x + p * hw;
+    const float* yp = y + p * hw;
+    float kp = 0.f, kq = 0.f, s1p = 0.f, s2p = 0.f, s1q = 0.f, s2q = 0.f, c = 0.f;
+    auto add = [&](float u, float v) {
+      const float a = u - kp, b = v - kq;
+      s1p += a;
+      s2p += a * a;
+      s1q += b;
+      s2q += b * b;
+    };
+    if (vec) {
+      const int64_t i0 = c0 + 4 * threadIdx.x;
+      if (i0 < c1) {
+        kp = xp[i0];
+        kq = yp[i0];
+      }
+#pragma unroll 4
+      for (int64_t i = i0; i < c1; i += 4 * kThreads) {
+        const float4 a = *reinterpret_cast<const float4*>(xp + i), b = *reinterpret_cast<const float4*>(yp + i);
+        add(a.x, b.x);
+        add(a.y, b.y);
+        add(a.z, b.z);
+        add(a.w, b.w);
+        c += 4.f;
+      }
+    } else {
+      const int64_t i0 = c0 + threadIdx.x;
+      if (i0 < c1) {
+        kp = xp[i0];
+        kq = yp[i0];
+      }
+      for (int64_t i = i0; i < c1; i += kThreads) {
+        add(xp[i], yp[i]);
+        c += 1.f;
+      }
+    }
+    Mom A{c, c > 0.f ? kp + s1p / c : 0.f, c > 0.f ? fmaxf(s2p - s1p * s1p / c, 0.f) : 0.f};
+    Mom B{c, c > 0.f ? kq + s1q / c : 0.f, c > 0.f ? fmaxf(s2q - s1q * s1q / c, 0.f) : 0.f};
+    A = mom_block(A, sh);
+    B = mom_block(B, sh);
+    if (threadIdx.x == 0) {
+      float* o = part + (p * nchunks + blockIdx.x) * 6;
+      o[0] = A.n;
+      o[1] = A.mean;
+      o[2] = A.m2;
+      o[3] = B.mean;
+      o[4] = B.m2;
+      o[5] = 0.f;
+    }
+  }
+}
+
+// The plane's moments from its chunk partials, merged in chunk order (every caller the same way).
+__device__ __forceinline__ void plane_moments(const float* __restrict__ part, int64_t p, int nchunks, int64_t hw,
+                                              float eps, float& mx, float& sx, float& my, float& sy) {
+  const float* q = part + p * nchunks * 6;
+  Mom A{q[0], q[1], q[2]}, B{q[0], q[3], q[4]};
+  for (int k = 1; k < nchunks; ++k) {
+    const float* r = q + 6 * k;
+    A = mom_merge(A, Mom{r[0], r[1], r[2]});
+    B = mom_merge(B, Mom{r[0], r[3], r[4]});
+  }
+  mx = A.mean;
+  sx = sqrtf(A.m2 / (float)(hw - 1) + eps);
+  my = B.mean;
+  sy = sqrtf(B.m2 / (float)(hw - 1) + eps);
+}
+
+__global__ __launch_bounds__(kThreads) void mvn_huber_part_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                                  int64_t planes, int64_t hw, int nchunks,
+                                                                  const float* __restrict__ part,
+                                                                  float* __restrict__ hpart, float* __restrict__ pstats) {
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk, c1 = min(hw, c0 + (int64_t)kChunk);
+  const bool vec = vec4_ok(x, y, hw);
+  for (int64_t p = blockIdx.y; p < planes; p += gridDim.y) {
+    float mx, sx, my, sy;
+    plane_moments(part, p, nchunks, hw, 1e-5f, mx, sx, my, sy);
+    const float* xp = x + p * hw;
+    const float* yp = y + p * hw;
+    float sh_ = 0.f, sg = 0.f, sgz = 0.f;
+    auto one = [&](float u, float v) {
+      const float z = (u - mx) / sx;
+      const float d = z - (v - my) / sy;
+      sh_ += huber(d);
+      const float g = huber_grad(d);
+      sg += g;
+      sgz += g * z;
+    };
+    if (vec) {
+#pragma unroll 4
+      for (int64_t i = c0 + 4 * threadIdx.x; i < c1; i += 4 * kThreads) {
+        const float4 a = *reinterpret_cast<const float4*>(xp + i), b = *reinterpret_cast<const float4*>(yp + i);
+        one(a.x, b.x);
+        one(a.y, b.y);
+        one(a.z, b.z);
+        one(a.w, b.w);
+      }
+    } else {
+      for (int64_t i = c0 + threadIdx.x; i < c1; i += kThreads) one(xp[i], yp[i]);
+    }
+    const float H = ast_det::block_sum_fixed(sh_);
+    const float G = ast_det::block_sum_fixed(sg);
+    const float GZ = ast_det::block_sum_fixed(sgz);
+    if (threadIdx.x == 0) {
+      float* o = hpart + (p * nchunks + blockIdx.x) * 4;
+      o[0] = H;
+      o[1] = G;
+      o[2] = GZ;
+      o[3] = 0.f;
+      if (pstats && blockIdx.x == 0) {
+        float* s = pstats + 6 * p;
+        s[0] = mx; s[1] = sx; s[2] = my; s[3] = sy;
+      }
+    }
+  }
+}
+
+// Per plane (one thread each): the chunk sums in chunk order -> pstats[4..5]; the Huber sums of the
+// workgroup's planes, in plane order, into the loss accumulator.
+__global__ __launch_bounds__(kThreads) void mvn_huber_fin_kernel(const float* __restrict__ hpart, int64_t planes,
+                                                                 int nchunks, int64_t hw, float inv_numel, float w,
+                                                                 float* loss, float* __restrict__ pstats) {
+  float Hs = 0.f;
+  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < planes; p += (int64_t)gridDim.x * kThreads) {
+    const float* q = hpart + p * nchunks * 4;
+    float H = 0.f, G = 0.f, GZ = 0.f;
+    for (int k = 0; k < nchunks; ++k) {
+      H += q[4 * k];
+      G += q[4 * k + 1];
+      GZ += q[4 * k + 2];
+    }
+    Hs += H;
+    if (pstats) {
+      pstats[6 * p + 4] = G / (float)hw;
+      pstats[6 * p + 5] = GZ / (float)(hw - 1);
+    }
+  }
+  const float t = ast_det::block_sum_fixed(Hs);
+  if (loss) ast_det::loss_acc_commit(loss, w * t * inv_numel);
+}
+
+// style_stats_kernel's (mu_x, sd_x, mu_y, sd_y) from the chunk partials (unbiased, no eps).
+__global__ __launch_bounds__(kThreads) void style_stats_fin_kernel(const float* __restrict__ part, int64_t planes,
+                                                                   int nchunks, int64_t hw, float* __restrict__ stats) {
+  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < planes; p += (int64_t)gridDim.x * kThreads) {
+    float mx, sx, my, sy;
+    plane_moments(part, p, nchunks, hw, 0.f, mx, sx, my, sy);
+    stats[4 * p + 0] = mx;
+    stats[4 * p + 1] = sx;
+    stats[4 * p + 2] = my;
+    stats[4 * p + 3] = sy;
+  }
+}
+
 // Backward of mean_variance_norm alone: dx = (g - mean(g) - z*sum(g z)/(N-1)) / sigma.
 __global__ __launch_bounds__(kThreads) void mvn_backward_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                                 float* __restrict__ dx, int64_t hw, float eps) {
@@ -574,6 +750,63 @@ int ast_mvn_huber_f32(const float* x, const float* y, long long planes, long lon
   const unsigned grid = (unsigned)std::min<long long>(planes, AST_LOSS_SLOTS);
   hipLaunchKernelGGL(mvn_huber_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, x, y, (int64_t)planes,
                      (int64_t)hw, (float)(1.0 / ((double)planes * hw)), weight, loss, pstats);
+  return (int)hipGetLastError();
+}
+
+long long ast_plane_stats_workspace_floats(long long planes, long long hw) {
+  if (planes <= 0 || hw <= 0) return 0;
+  return planes * ((hw + kChunk - 1) / kChunk) * 10;
+}
+
+// part / hpart of the split-plane kernels inside the caller's workspace
+static int plane_split_plan(long long planes, long long hw, float* ws, long long ws_floats, int* nchunks,
+                            unsigned* gy) {
+  if (!ws) return AST_E_NULLPTR;
+  if (ws_floats < ast_plane_stats_workspace_floats(planes, hw)) return AST_E_SHAPE;
+  const long long nc = (hw + kChunk - 1) / kChunk;
+  if (nc > 0x7fffffffLL) return AST_E_SHAPE;
+  *nchunks = (int)nc;
+  *gy = (unsigned)std::min<long long>(planes, 65535);
+  return AST_OK;
+}
+
+int ast_mvn_huber_ws_f32(const float* x, const float* y, long long planes, long long hw, float weight, float* loss,
+                         float* pstats, float* workspace, long long workspace_floats, void* stream) {
+  if (!x || !y) return AST_E_NULLPTR;
+  if (planes <= 0 || hw <= 1 || planes > 0x7fffffffLL) return AST_E_SHAPE;
+  int nc = 0;
+  unsigned gy = 0;
+  const int e = plane_split_plan(planes, hw, workspace, workspace_floats, &nc, &gy);
+  if (e != AST_OK) return e;
+  hipStream_t s = (hipStream_t)stream;
+  float* part = workspace;
+  float* hpart = workspace + planes * nc * 6;
+  hipLaunchKernelGGL(moments_part_kernel, dim3((unsigned)nc, gy), dim3(kThreads), 0, s, x, y, (int64_t)planes,
+                     (int64_t)hw, nc, part);
+  hipLaunchKernelGGL(mvn_huber_part_kernel, dim3((unsigned)nc, gy), dim3(kThreads), 0, s, x, y, (int64_t)planes,
+                     (int64_t)hw, nc, part, hpart, pstats);
+  hipLaunchKernelGGL(mvn_huber_fin_kernel, dim3(grid_for(planes)), dim3(kThreads), 0, s, hpart, (int64_t)planes, nc,
+                     (int64_t)hw, (float)(1.0 / ((double)planes * hw)), weight, loss, pstats);
+  return (int)hipGetLastError();
+}
+
+int ast_style_moments_ws_f32(const float* x, const float* y, long long planes, long long hw, float weight,
+                             const float* gscale, float* stats, float* loss, float* row_a, float* row_b,
+                             float* workspace, long long workspace_floats, void* stream) {
+  if (!x || !y || !stats) return AST_E_NULLPTR;
+  if ((row_a == nullptr) != (row_b == nullptr)) return AST_E_NULLPTR;
+  if (planes <= 0 || hw <= 0 || planes > 0x7fffffffLL) return AST_E_SHAPE;
+  int nc = 0;
+  unsigned gy = 0;
+  const int e = plane_split_plan(planes, hw, workspace, workspace_floats, &nc, &gy);
+  if (e != AST_OK) return e;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(moments_part_kernel, dim3((unsigned)nc, gy), dim3(kThreads), 0, s, x, y, (int64_t)planes,
+                     (int64_t)hw, nc, workspace);
+  hipLaunchKernelGGL(style_stats_fin_kernel, dim3(grid_for(planes)), dim3(kThreads), 0, s, workspace, (int64_t)planes,
+                     nc, (int64_t)hw, stats);
+  hipLaunchKernelGGL(style_moment_loss_kernel, dim3(grid_for(planes)), dim3(kThreads), 0, s, stats, (int64_t)planes,
+                     (int64_t)hw, weight, gscale, loss, row_a, row_b);
   return (int)hipGetLastError();
 }
 

@@ -4,6 +4,8 @@ backward on the GPU through the same C ABI (no PyTorch compute on the path).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import ops
@@ -340,6 +342,24 @@ class HuberFn(torch.autograd.Function):
         return dx, dy
 
 
+# the content / style-moment losses' split-plane launches (AST_PLANE_SPLIT=0: one workgroup per
+# plane, the round-2 kernels; kept for A/B measurement)
+PLANE_SPLIT = os.environ.get("AST_PLANE_SPLIT", "1") == "1"
+
+
+def mvn_huber(x, y, weight, loss, pstats):
+    """loss += weight * compute_content_loss(mvn(x), mvn(y)); pstats (or None) for the backward.
+    The split-plane launch (chunk partials merged in order through a workspace)."""
+    n, c = int(x.shape[0]), int(x.shape[1])
+    hw = x[0, 0].numel()
+    if not PLANE_SPLIT:
+        check(lib().ast_mvn_huber_f32(ptr(x), ptr(y), n * c, hw, weight, ptr(loss), ptr(pstats), _s(x)), "mvn_huber")
+        return
+    ws = workspace(lib().ast_plane_stats_workspace_floats(n * c, hw), x.device)
+    check(lib().ast_mvn_huber_ws_f32(ptr(x), ptr(y), n * c, hw, weight, ptr(loss), ptr(pstats), ptr(ws), ws.numel(),
+                                     _s(x)), "mvn_huber")
+
+
 class MVNHuberFn(torch.autograd.Function):
     """compute_content_loss(mean_variance_norm(x), mean_variance_norm(y)) with y detached (as
     every call site in train.py), one fused kernel for value and gradient."""
@@ -352,8 +372,7 @@ class MVNHuberFn(torch.autograd.Function):
         n, c = x.shape[:2]
         loss = _acc(x)
         pstats = _empty((n * c, 6), x) if ctx.needs_input_grad[0] else None
-        check(lib().ast_mvn_huber_f32(ptr(x), ptr(y), n * c, x[0, 0].numel(), weight, ptr(loss), ptr(pstats),
-                                      _s(x)), "mvn_huber")
+        mvn_huber(x, y, weight, loss, pstats)
         ctx.save_for_backward(x, y, pstats)
         ctx.weight = weight
         return _value(loss)
@@ -409,8 +428,13 @@ def _style_terms(x, y, weight, loss, want_grad):
     s = _s(x)
     if y.shape[2:] != x.shape[2:]:
         raise HipOpError("style loss: feature maps must have the same spatial size")
-    check(L.ast_style_moments_f32(ptr(x), ptr(y), planes, hw, weight, None, ptr(stats), ptr(loss), ptr(ra),
-                                  ptr(rb), s), "style_moments")
+    if not PLANE_SPLIT:
+        check(L.ast_style_moments_f32(ptr(x), ptr(y), planes, hw, weight, None, ptr(stats), ptr(loss), ptr(ra),
+                                      ptr(rb), s), "style_moments")
+    else:
+        ws = workspace(L.ast_plane_stats_workspace_floats(planes, hw), x.device)
+        check(L.ast_style_moments_ws_f32(ptr(x), ptr(y), planes, hw, weight, None, ptr(stats), ptr(loss), ptr(ra),
+                                         ptr(rb), ptr(ws), ws.numel(), s), "style_moments")
     gx = _empty((b, c, c), x)
     gy = _empty((b, c, c), x)
     scale = 1.0 / (c * hw)

@@ -206,8 +206,7 @@ def content_mvn_loss(x: Tensor, y: Tensor, weight: float, want_grad: bool) -> Tu
     n, c = x.shape[:2]
     acc = _acc(x)
     pstats = torch.empty((n * c, 6), device=x.device) if want_grad else _empty(x)
-    check(lib().ast_mvn_huber_f32(ptr(x), ptr(y), n * c, x[0, 0].numel(), weight, ptr(acc),
-                                  ptr(pstats) if want_grad else None, stream_ptr(x.device)), "mvn_huber")
+    Fn.mvn_huber(x, y, weight, acc, pstats if want_grad else None)
     return acc[0], pstats
 
 

@@ -204,6 +204,14 @@ int ast_gram_backward_f32(const float* feat, const float* dgram, float* dfeat,
 int ast_mvn_huber_f32(const float* x, const float* y, long long planes, long long hw, float weight,
                       float* loss, float* pstats, void* stream);
 
+/* The same, split over (chunk, plane) workgroups: partial moments and Huber sums of each chunk of
+ * 8192 elements go to `workspace` (ast_plane_stats_workspace_floats(planes, hw) floats) and are
+ * merged in chunk order, so few large planes fill the chip. Three launches; same outputs. */
+long long ast_plane_stats_workspace_floats(long long planes, long long hw);
+int ast_mvn_huber_ws_f32(const float* x, const float* y, long long planes, long long hw, float weight,
+                         float* loss, float* pstats, float* workspace, long long workspace_floats,
+                         void* stream);
+
 /* d/dx of the above (y constant), from the forward's pstats: one pass over x and y. */
 int ast_mvn_huber_backward_f32(const float* x, const float* y, const float* pstats, long long planes,
                                long long hw, float weight, const float* gscale, float* dx,
@@ -220,6 +228,12 @@ int ast_huber_f32(const float* x, const float* y, long long n, float weight, con
 int ast_style_moments_f32(const float* x, const float* y, long long planes, long long hw, float weight,
                           const float* gscale, float* stats, float* loss, float* row_a, float* row_b,
                           void* stream);
+
+/* The same with the plane moments split over (chunk, plane) workgroups through `workspace`
+ * (ast_plane_stats_workspace_floats(planes, hw) floats; merged in chunk order). */
+int ast_style_moments_ws_f32(const float* x, const float* y, long long planes, long long hw, float weight,
+                             const float* gscale, float* stats, float* loss, float* row_a, float* row_b,
+                             float* workspace, long long workspace_floats, void* stream);
 
 /* Gram part of compute_style_loss (losses.py:135-137): loss += weight * 10 * mean(huber(gx-gy)),
  * dgram = d/dgx (NULL: value only). */

@@ -189,6 +189,39 @@ def test_style_loss_vs_oracle(shape, hip_device):
     assert rel_inf(xd.grad, xr.grad) <= TOL
 
 
+@pytest.mark.parametrize("shape,offset", [((16, 3, 512, 512), 0), ((1, 2, 300, 300), 0), ((2, 3, 37, 41), 0),
+                                          ((4, 8, 96, 96), 1), ((3, 64, 64, 64), 0)])
+def test_plane_stats_losses_vs_oracle(shape, offset, hip_device):
+    """The split-plane content (mvn + Huber) and style-moment losses: planes cut into 8192-element
+    chunks (one partial chunk, several chunks, unaligned planes -> 4-byte path), chunk partials
+    merged in order; value and gradient against float64 (losses.py:124-139, models.py:64-68)."""
+    n = int(np.prod(shape))
+    x = rnd(71, (n + offset,), 1.3, 0.2)[offset:].reshape(shape)
+    y = rnd(72, (n + offset,), 0.9, 0.5)[offset:].reshape(shape)
+    xr = x.double().requires_grad_()
+    cref = R.compute_content_loss(R.mean_variance_norm(xr), R.mean_variance_norm(y.double())) * 0.7
+    cref.backward()
+    xs = torch.empty(n + offset, device=hip_device)[offset:].view(shape)   # same (mis)alignment on the device
+    xs.copy_(x)
+    ys = torch.empty(n + offset, device=hip_device)[offset:].view(shape)
+    ys.copy_(y)
+    xd = xs.detach().requires_grad_()
+    got = L.content_mvn_loss(xd, ys, 0.7)
+    got.backward()
+    np.testing.assert_allclose(got.item(), cref.item(), rtol=2e-5)
+    assert rel_inf(xd.grad, xr.grad) <= TOL
+    again = L.content_mvn_loss(xs, ys, 0.7)
+    assert torch.equal(again, got.detach())   # chunk partials merged in a fixed order
+    xr.grad = None
+    sref = R.compute_style_loss(xr, y.double()) * 0.75
+    sref.backward()
+    xd.grad = None
+    got = L.style_loss_weighted(xd, ys, 0.75)
+    got.backward()
+    np.testing.assert_allclose(got.item(), sref.item(), rtol=2e-5)
+    assert rel_inf(xd.grad, xr.grad) <= TOL
+
+
 @pytest.mark.parametrize("canonical,alpha,style_hw", [(False, 1.0, (6, 6)), (True, 0.6, (6, 6)), (False, 0.3, (9, 5))])
 def test_adain_backward(canonical, alpha, style_hw, hip_device):
     c = rnd(61, (2, 8, 6, 6), 2.0, 0.5)
