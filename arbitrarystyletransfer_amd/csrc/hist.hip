@@ -264,7 +264,7 @@ int ast_range_loss_f32(const float* x, long long numel, float weight, const floa
                        int accumulate, void* stream) {
   if (!x || (!loss && !dx)) return AST_E_NULLPTR;
   if (numel <= 0) return AST_E_SHAPE;
-  hipLaunchKernelGGL(range_loss_kernel, dim3(grid_for(numel, 4 * kThreads)), dim3(kThreads), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(range_loss_kernel, dim3(std::min(grid_for(numel, 4 * kThreads), 256u)), dim3(kThreads), 0, (hipStream_t)stream,
                      x, (int64_t)numel, weight / (float)numel, gscale, loss, dx, accumulate);
   return (int)hipGetLastError();
 }
@@ -273,7 +273,7 @@ int ast_sqdiff_mean_f32(const float* x, const float* y, long long numel, float w
                         float* loss, float* dx, int accumulate, void* stream) {
   if (!x || !y || (!loss && !dx)) return AST_E_NULLPTR;
   if (numel <= 0) return AST_E_SHAPE;
-  hipLaunchKernelGGL(sqdiff_kernel, dim3(grid_for(numel, 4 * kThreads)), dim3(kThreads), 0, (hipStream_t)stream, x,
+  hipLaunchKernelGGL(sqdiff_kernel, dim3(std::min(grid_for(numel, 4 * kThreads), 256u)), dim3(kThreads), 0, (hipStream_t)stream, x,
                      y, (int64_t)numel, weight / (float)numel, gscale, loss, dx, accumulate);
   return (int)hipGetLastError();
 }

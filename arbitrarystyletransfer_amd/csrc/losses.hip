@@ -174,10 +174,11 @@ __global__ __launch_bounds__(kThreads) void mvn_huber_bwd_kernel(const float* __
     const float* xp = x + p * hw;
     const float* yp = y + p * hw;
     float* dp = dx + p * hw;
+    const float i1 = 1.f / s1, i3 = 1.f / s3, c1 = cc * i1;
     auto one = [&](float xv, float yv) {
-      const float z = (xv - s0) / s1;
-      const float d = z - (yv - s2) / s3;
-      return cc * (huber_grad(d) - s4 - z * s5) / s1;
+      const float z = (xv - s0) * i1;
+      const float d = z - (yv - s2) * i3;
+      return c1 * (huber_grad(d) - s4 - z * s5);
     };
     for (int64_t i = ((int64_t)blockIdx.x * kThreads + threadIdx.x) * 4; i < hw; i += (int64_t)gridDim.x * kThreads * 4) {
       if (vec) {
@@ -300,9 +301,10 @@ __global__ __launch_bounds__(kThreads) void mvn_huber_part_kernel(const float* _
     const float* xp = x + p * hw;
     const float* yp = y + p * hw;
     float sh_ = 0.f, sg = 0.f, sgz = 0.f;
+    const float isx = 1.f / sx, isy = 1.f / sy;  // two divisions per element made this pass VALU-bound
     auto one = [&](float u, float v) {
-      const float z = (u - mx) / sx;
-      const float d = z - (v - my) / sy;
+      const float z = (u - mx) * isx;
+      const float d = z - (v - my) * isy;
       sh_ += huber(d);
       const float g = huber_grad(d);
       sg += g;
@@ -543,45 +545,66 @@ __global__ __launch_bounds__(256) void gram_kernel(const float* __restrict__ F, 
   const float* Fb = F + (int64_t)b * C * K;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   const int wi = wave & 1, wj = wave >> 1;
+  // a diagonal tile reads its rows once (both operands from As), and its lower-left 32x32 quadrant,
+  // which is never stored (the mirror of the upper-right one), is not computed
+  const bool diag = ti == tj, idle = diag && wi > wj;
+  const float(*Bp)[GT + 4] = diag ? As : Bs;
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const bool vec = ((K & 3) == 0) && ((k0 & 3) == 0);
-  for (int64_t kb = k0; kb < k1; kb += GBK) {
-    // 64 rows x 32 k for each operand: 512 float4 each -> 2 per thread per operand
+  // 64 rows x 32 k for each operand: 512 float4 each -> 2 per thread per operand, the next chunk's
+  // in registers while the current one's MFMAs run
+  float4 va[2], vb[2];
+  auto load = [&](int64_t kb) {
 #pragma unroll
     for (int rep = 0; rep < 2; ++rep) {
       const int e = tid + rep * 256;  // 0..511
       const int row = e >> 3, kq = (e & 7) * 4;
       const int ri = ti * GT + row, rj = tj * GT + row;
-      float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+      va[rep] = make_float4(0.f, 0.f, 0.f, 0.f);
+      vb[rep] = va[rep];
       const int64_t kk = kb + kq;
       if (vec && kk + 3 < k1) {
-        if (ri < C) va = *reinterpret_cast<const float4*>(Fb + (int64_t)ri * K + kk);
-        if (rj < C) vb = *reinterpret_cast<const float4*>(Fb + (int64_t)rj * K + kk);
+        if (ri < C) va[rep] = *reinterpret_cast<const float4*>(Fb + (int64_t)ri * K + kk);
+        if (!diag && rj < C) vb[rep] = *reinterpret_cast<const float4*>(Fb + (int64_t)rj * K + kk);
       } else {
         float ta[4] = {0.f, 0.f, 0.f, 0.f}, tb[4] = {0.f, 0.f, 0.f, 0.f};
         for (int q = 0; q < 4; ++q) {
           if (kk + q < k1) {
             if (ri < C) ta[q] = Fb[(int64_t)ri * K + kk + q];
-            if (rj < C) tb[q] = Fb[(int64_t)rj * K + kk + q];
+            if (!diag && rj < C) tb[q] = Fb[(int64_t)rj * K + kk + q];
           }
         }
-        va = make_float4(ta[0], ta[1], ta[2], ta[3]);
-        vb = make_float4(tb[0], tb[1], tb[2], tb[3]);
+        va[rep] = make_float4(ta[0], ta[1], ta[2], ta[3]);
+        vb[rep] = make_float4(tb[0], tb[1], tb[2], tb[3]);
       }
-      As[kq + 0][row] = va.x; As[kq + 1][row] = va.y; As[kq + 2][row] = va.z; As[kq + 3][row] = va.w;
-      Bs[kq + 0][row] = vb.x; Bs[kq + 1][row] = vb.y; Bs[kq + 2][row] = vb.z; Bs[kq + 3][row] = vb.w;
+    }
+  };
+  if (k0 < k1) load(k0);
+  for (int64_t kb = k0; kb < k1; kb += GBK) {
+#pragma unroll
+    for (int rep = 0; rep < 2; ++rep) {
+      const int e = tid + rep * 256;
+      const int row = e >> 3, kq = (e & 7) * 4;
+      As[kq + 0][row] = va[rep].x; As[kq + 1][row] = va[rep].y; As[kq + 2][row] = va[rep].z; As[kq + 3][row] = va[rep].w;
+      if (!diag) {
+        Bs[kq + 0][row] = vb[rep].x; Bs[kq + 1][row] = vb[rep].y; Bs[kq + 2][row] = vb[rep].z; Bs[kq + 3][row] = vb[rep].w;
+      }
     }
     __syncthreads();
+    if (kb + GBK < k1) load(kb + GBK);
+    if (!idle) {
 #pragma unroll
-    for (int kp = 0; kp < GBK / 2; ++kp) {
-      const float a = As[2 * kp + h][wi * 32 + l32];
-      const float bv = Bs[2 * kp + h][wj * 32 + l32];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc, 0, 0, 0);
+      for (int kp = 0; kp < GBK / 2; ++kp) {
+        const float a = As[2 * kp + h][wi * 32 + l32];
+        const float bv = Bp[2 * kp + h][wj * 32 + l32];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc, 0, 0, 0);
+      }
     }
     __syncthreads();
   }
+  if (idle) return;
   float* Gb = G + ((int64_t)blockIdx.y * gridDim.z + b) * C * C;
   const int j = tj * GT + wj * 32 + l32;
 #pragma unroll
@@ -616,16 +639,17 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
   for (int q = 0; q < 2; ++q)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
-  for (int k0 = 0; k0 < C; k0 += BBK) {
+  // the next k-chunk's S and F values in registers while the current chunk's MFMAs run
+  float sv[4];
+  float4 fv[2];
+  auto load = [&](int k0) {
     // S tile: 16 k x 64 i = 1024 entries, 4 per thread
 #pragma unroll
     for (int rep = 0; rep < 4; ++rep) {
       const int e = tid + rep * 256;
       const int kk = e >> 6, ii = e & 63;
       const int k = k0 + kk, i = ti * BI + ii;
-      float v = 0.f;
-      if (k < C && i < C) v = dGb[(int64_t)k * C + i] + dGb[(int64_t)i * C + k];
-      As[kk][ii] = v;
+      sv[rep] = (k < C && i < C) ? dGb[(int64_t)k * C + i] + dGb[(int64_t)i * C + k] : 0.f;
     }
     // F tile: 16 k x 128 n = 512 float4 -> 2 per thread
 #pragma unroll
@@ -645,9 +669,23 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
           v = make_float4(t[0], t[1], t[2], t[3]);
         }
       }
-      *reinterpret_cast<float4*>(&Bs[kk][nq]) = v;
+      fv[rep] = v;
+    }
+  };
+  load(0);
+  for (int k0 = 0; k0 < C; k0 += BBK) {
+#pragma unroll
+    for (int rep = 0; rep < 4; ++rep) {
+      const int e = tid + rep * 256;
+      As[e >> 6][e & 63] = sv[rep];
+    }
+#pragma unroll
+    for (int rep = 0; rep < 2; ++rep) {
+      const int e = tid + rep * 256;
+      *reinterpret_cast<float4*>(&Bs[e >> 5][(e & 31) * 4]) = fv[rep];
     }
     __syncthreads();
+    if (k0 + BBK < C) load(k0 + BBK);
 #pragma unroll
     for (int kp = 0; kp < BBK / 2; ++kp) {
       const float a = As[2 * kp + h][wi * 32 + l32];
@@ -679,6 +717,14 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
 }
 
 int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, AST_LOSS_SLOTS)); }
+
+// Grid of an elementwise loss kernel that commits to a loss accumulator: every workgroup's commit
+// is an agent-scope release (an L2 writeback on the multi-XCD part), measured at ~25 ns per
+// workgroup (gram_huber over 4096 workgroups: 104 us for 50 MB) -- so at most 256, looping (1024
+// for tv_kernel, whose per-element index math makes long loops slower than the commits).
+int loss_grid(int64_t n, int64_t cap = 256) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, cap));
+}
 
 }  // namespace
 
@@ -846,7 +892,7 @@ int ast_huber_f32(const float* x, const float* y, long long n, float weight, con
                   float* dx, int accumulate, void* stream) {
   if (!x || !y) return AST_E_NULLPTR;
   if (n <= 0) return AST_E_SHAPE;
-  hipLaunchKernelGGL(huber_kernel, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, x, y, (int64_t)n,
+  hipLaunchKernelGGL(huber_kernel, dim3(loss_grid(n)), dim3(kThreads), 0, (hipStream_t)stream, x, y, (int64_t)n,
                      (float)(1.0 / (double)n), weight, gscale, loss, dx, accumulate ? 1 : 0);
   return (int)hipGetLastError();
 }
@@ -867,7 +913,7 @@ int ast_gram_huber_f32(const float* gx, const float* gy, long long n, float weig
                        float* dgram, void* stream) {
   if (!gx || !gy) return AST_E_NULLPTR;
   if (n <= 0) return AST_E_SHAPE;
-  hipLaunchKernelGGL(gram_huber_kernel, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, gx, gy,
+  hipLaunchKernelGGL(gram_huber_kernel, dim3(loss_grid(n)), dim3(kThreads), 0, (hipStream_t)stream, gx, gy,
                      (int64_t)n, weight, gscale, loss, dgram);
   return (int)hipGetLastError();
 }
@@ -876,7 +922,7 @@ int ast_tv_loss_f32(const float* x, long long planes, int h, int w, float weight
                     float* dx, int accumulate, void* stream) {
   if (!x) return AST_E_NULLPTR;
   if (planes <= 0 || h <= 0 || w <= 0) return AST_E_SHAPE;
-  hipLaunchKernelGGL(tv_kernel, dim3(grid_for(planes * h * w)), dim3(kThreads), 0, (hipStream_t)stream, x,
+  hipLaunchKernelGGL(tv_kernel, dim3(loss_grid(planes * h * w, 1024)), dim3(kThreads), 0, (hipStream_t)stream, x,
                      (int64_t)planes, h, w, weight, gscale, loss, dx, accumulate ? 1 : 0);
   return (int)hipGetLastError();
 }

@@ -271,6 +271,64 @@ def _style_backward(ctx, g, *_):
 register_autograd("ast_hip::style_loss", _style_backward, setup_context=_style_setup)
 
 
+@custom_op("ast_hip::content_style_loss", mutates_args=())
+def content_style_loss(x: Tensor, yc: Tensor, ys: Tensor, wc: float, ws: float,
+                       want_grad: bool) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """(wc * content_mvn_loss(x, yc), ws * compute_style_loss(x, ys)) of ONE feature map x (the
+    trainers apply both to every loss tap, train.py:217-245): the backward writes dx once -- the
+    Gram-backward GEMM, then the content gradient added in place (the same fp32 sum autograd's add
+    of the two gradients made, one read-modify-write of dx fewer). Extra outputs: the backward's
+    state (pstats, dG, row_a, row_b; empty unless want_grad)."""
+    n, c = x.shape[:2]
+    acc_c, acc_s = _acc(x), _acc(x)
+    pstats = torch.empty((n * c, 6), device=x.device) if want_grad else None
+    Fn.mvn_huber(x, yc, wc, acc_c, pstats)
+    dg, ra, rb = Fn._style_terms(x, ys, ws, acc_s, want_grad=want_grad)
+    e = lambda t: t if t is not None else _empty(x)  # noqa: E731
+    return acc_c[0], acc_s[0], e(pstats), e(dg), e(ra), e(rb)
+
+
+@register_fake("ast_hip::content_style_loss")
+def _(x, yc, ys, wc, ws, want_grad):
+    b, c = x.shape[:2]
+    if want_grad:
+        return (x.new_empty(()), x.new_empty(()), x.new_empty((b * c, 6)), x.new_empty((b, c, c)),
+                x.new_empty((b * c,)), x.new_empty((b * c,)))
+    return (x.new_empty(()), x.new_empty(()), x.new_empty((0,)), x.new_empty((0,)), x.new_empty((0,)),
+            x.new_empty((0,)))
+
+
+def _cs_setup(ctx, inputs, output):
+    x, yc, ys, wc, ws, want_grad = inputs
+    if not want_grad:
+        raise NotImplementedError("ast_hip::content_style_loss under autograd needs want_grad=True")
+    ctx.save_for_backward(x, yc, output[2], output[3], output[4], output[5])
+    ctx.wc = wc
+
+
+def _cs_backward(ctx, gc, gs, *_):
+    x, yc, pstats, dg, ra, rb = ctx.saved_tensors
+    b, c, h, w = x.shape
+    st = stream_ptr(x.device)
+    dx = torch.empty_like(x)
+    first = True
+    if gs is not None:
+        check(lib().ast_gram_backward_f32(ptr(x), ptr(dg), ptr(dx), ptr(ra), ptr(rb), b, c, h * w, 1.0 / (c * h * w),
+                                          ptr(gs.contiguous()), 0, st), "gram_backward")
+        first = False
+    if gc is not None:
+        check(lib().ast_mvn_huber_backward_f32(ptr(x), ptr(yc), ptr(pstats), b * c, h * w, ctx.wc,
+                                               ptr(gc.contiguous()), ptr(dx), 0 if first else 1, st),
+              "mvn_huber_backward")
+        first = False
+    if first:
+        dx.zero_()
+    return dx, None, None, None, None, None
+
+
+register_autograd("ast_hip::content_style_loss", _cs_backward, setup_context=_cs_setup)
+
+
 @custom_op("ast_hip::huber_loss", mutates_args=())
 def huber_loss(x: Tensor, y: Tensor) -> Tensor:
     acc = _acc(x)

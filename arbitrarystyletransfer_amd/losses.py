@@ -27,7 +27,8 @@ def _pair(x, y, what):
     return x, y
 
 __all__ = ["gram_matrix", "compute_content_loss", "compute_style_loss", "tv_loss", "compute_hist_loss",
-           "content_mvn_loss", "style_loss_weighted", "EarthMoversDistanceLoss", "HistLayerBase",
+           "content_mvn_loss", "style_loss_weighted", "content_style_loss", "EarthMoversDistanceLoss",
+           "HistLayerBase",
            "SingleDimHistLayer", "hist", "earth_movers", "out_of_range_loss", "pixel_mse_loss"]
 
 
@@ -57,6 +58,19 @@ def content_mvn_loss(inp, tgt, weight: float = 1.0):
     in one fused kernel (train.py:223-227, 258, 277)."""
     x, y = _pair(inp, tgt.detach(), "content loss")
     return _ops.content_mvn_loss(x, y, float(weight), _grad(x))[0]
+
+
+def content_style_loss(inp, content_tgt, style_tgt, content_weight: float = 1.0, style_weight: float = 1.0):
+    """(content_weight * content_mvn_loss(inp, content_tgt), style_weight * compute_style_loss(inp,
+    style_tgt)) -- the pair the trainers take at every loss tap (train.py:217-245, 258, 271), with
+    the input gradient formed in one buffer (library.content_style_loss)."""
+    x = _dev(inp, "x")
+    yc, ys = _dev(content_tgt.detach(), "content target"), _dev(style_tgt.detach(), "style target")
+    if x.shape != yc.shape or x.shape != ys.shape:
+        raise Fn.HipOpError(f"content/style loss: shape mismatch {tuple(x.shape)} vs {tuple(yc.shape)}, "
+                            f"{tuple(ys.shape)}")
+    out = _ops.content_style_loss(x, yc, ys, float(content_weight), float(style_weight), _grad(x))
+    return out[0], out[1]
 
 
 def style_loss_weighted(t_cs_map, style_map, weight: float = 1.0):

@@ -162,10 +162,12 @@ class AdaINTrainer:
             enc_stylized = s_taps[_RELU9].detach() if self.shared else self.net.encoder(stylized.detach())[0]
             lf_loss = L.content_mvn_loss(t, enc_stylized)
 
-        content_terms = [L.content_mvn_loss(t_cs_map[i], content_map[i]) for i in range(len(t_cs_map))]
-        content_terms.append(L.content_mvn_loss(stylized, content, 0.1))
-        style_terms = [L.style_loss_weighted(t_cs_map[i], style_map[i], STYLE_WEIGHTS[i]) for i in range(len(t_cs_map))]
-        style_terms.append(L.style_loss_weighted(stylized, style, 1.0))
+        # content and style terms of each tap (and of the image) from one op: one input gradient each
+        pairs = [L.content_style_loss(t_cs_map[i], content_map[i], style_map[i], 1.0, STYLE_WEIGHTS[i])
+                 for i in range(len(t_cs_map))]
+        pairs.append(L.content_style_loss(stylized, content, style, 0.1, 1.0))
+        content_terms = [p[0] for p in pairs]
+        style_terms = [p[1] for p in pairs]
         tv = L.tv_loss(stylized)
         content_loss = torch.stack(content_terms).sum()
         style_loss = torch.stack(style_terms).sum()
@@ -327,10 +329,12 @@ class ASTTrainer:
             enc_stylized = self.ast._enc(stylized.detach(), out_layers=enc_out_layers)
         t_cs_map = self.pretrained_enc(stylized)                                        # :195
         org_out_map = self.pretrained_enc(org_out)                                      # :196
-        content_terms = [L.content_mvn_loss(x, y) for x, y in zip(t_cs_map, content_map)]              # :217-227
-        content_terms.append(L.content_mvn_loss(stylized, content, 0.1))                               # :258
-        style_terms = [L.style_loss_weighted(x, y, w) for x, y, w in zip(t_cs_map, style_map, STYLE_WEIGHTS)]  # :230-245
-        style_terms.append(L.style_loss_weighted(stylized, style, 1.0))                                # :271
+        # :217-227 content and :230-245 style terms per tap, :258 / :271 on the image, pairwise fused
+        pairs = [L.content_style_loss(x, yc, ys, 1.0, w) for x, yc, ys, w in zip(t_cs_map, content_map, style_map,
+                                                                                STYLE_WEIGHTS)]
+        pairs.append(L.content_style_loss(stylized, content, style, 0.1, 1.0))
+        content_terms = [p[0] for p in pairs]
+        style_terms = [p[1] for p in pairs]
         org_terms = [L.compute_content_loss(x, y) for x, y in zip(org_out_map, content_map)]           # :248-256
         org_terms.append(L.pixel_mse_loss(org_out, content, 100.0))                                    # :268
         content_loss = torch.stack(content_terms).sum()

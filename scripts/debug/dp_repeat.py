@@ -28,6 +28,9 @@ for it in range(runs):
         print(r.stdout[-2000:], r.stderr[-2000:])
         sys.exit(1)
     got = dict(np.load(out))
+    import hashlib
+    h = hashlib.sha1(b"".join(np.ascontiguousarray(got[k]).tobytes() for k in sorted(got) if k.startswith("grad:")))
+    print(f"run {it}: CUs {got.pop('cus', '?')} arch {got.pop('gcn', '?')} grad sha1 {h.hexdigest()[:16]}", flush=True)
     norm = float(got["grad_norm"])
     worst, wk = 0.0, None
     for key in golden.files:
@@ -45,3 +48,9 @@ for it in range(runs):
     else:
         diff = [k for k in got if not np.array_equal(got[k], first[k])]
     print(f"run {it}: worst {worst:.3e} ({wk}); keys differing from run 0: {len(diff)} {diff[:6]}", flush=True)
+    for k in diff[:40]:
+        a, b = np.asarray(got[k], np.float64), np.asarray(first[k], np.float64)
+        d = np.abs(a - b)
+        print(f"   {k} shape {a.shape}: max|d| {d.max():.3e} rel {d.max() / max(np.abs(b).max(), 1e-30):.3e} "
+              f"elements differing {int((d > 0).sum())}/{d.size} first at {np.unravel_index(int(np.argmax(d > 0)), d.shape)}",
+              flush=True)

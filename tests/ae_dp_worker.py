@@ -20,6 +20,12 @@ def main(out_path):
     g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ae_train_step_64.npz"))
     content = torch.from_numpy(g["content"])
     a, b = dp.shard_range(content.shape[0], rank, world)
+    poison = os.environ.get("AST_POISON")
+    if poison:   # debugging aid: fill the caching allocator's free blocks so unwritten reads show
+        big = [torch.full((1 << 28,), float(poison), device="cuda:0") for _ in range(4)]
+        mid = [torch.full((1 << 22,), float(poison), device="cuda:0") for _ in range(64)]
+        small = [torch.full((1 << 16,), float(poison), device="cuda:0") for _ in range(1024)]
+        del big, mid, small
     tr = AutoencoderTrainer(default_ae_args(batch_size=content.shape[0]), device="cuda:0", model=models.AutoEncoder().load_live_init())
     assert tr.grad_arena is not None
     snap = {}
@@ -30,11 +36,6 @@ def main(out_path):
         orig()
 
     tr.ae_optim.step = step
-    poison = os.environ.get("AST_POISON")
-    if poison:   # debugging aid: fill the caching allocator's free blocks so unwritten reads show
-        big = [torch.full((1 << 28,), float(poison), device="cuda:0") for _ in range(4)]
-        small = [torch.full((1 << 18,), float(poison), device="cuda:0") for _ in range(256)]
-        del big, small
     out = tr.train_step(content[a:b].cuda())
     losses = torch.stack([out[k].detach().float() for k in ("recon_loss", "content_loss", "loss")]).cpu()
     dist.all_reduce(losses)
@@ -42,7 +43,9 @@ def main(out_path):
     recon = [torch.zeros_like(out["recon"]).cpu() for _ in range(world)]
     dist.all_gather(recon, out["recon"].detach().cpu().contiguous())
     if rank == 0:
-        res = {"losses": losses.numpy(), "recon": torch.cat(recon).numpy(), "grad_norm": float(out["grad_norm"])}
+        props = torch.cuda.get_device_properties(0)
+        res = {"losses": losses.numpy(), "recon": torch.cat(recon).numpy(), "grad_norm": float(out["grad_norm"]),
+               "cus": props.multi_processor_count, "gcn": str(getattr(props, "gcnArchName", ""))}
         for n, p in tr.model.named_parameters():
             res[f"grad:{n}"] = snap[n].cpu().numpy()
             res[f"param:{n}"] = p.detach().cpu().numpy()

@@ -318,6 +318,9 @@ def test_autoencoder_dp_syncbn_step_golden(tmp_path):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     got = np.load(out)
+    if os.environ.get("AST_TEST_DUMP"):   # debugging aid: keep the ranks' result for offline diffing
+        import shutil
+        shutil.copy(out, os.path.join(os.environ["AST_TEST_DUMP"], f"dp_{os.getpid()}_{port}.npz"))
     g = np.load(GOLDEN)
     for i, k in enumerate(("recon_loss", "content_loss", "loss")):
         np.testing.assert_allclose(got["losses"][i], float(g[k]), rtol=1e-4, err_msg=k)

@@ -222,6 +222,23 @@ def test_plane_stats_losses_vs_oracle(shape, offset, hip_device):
     assert rel_inf(xd.grad, xr.grad) <= TOL
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 40, 36), (3, 3, 33, 17)])
+def test_content_style_pair_equals_separate_terms(shape, hip_device):
+    """content_style_loss (both terms of one tap, one input-gradient buffer) is bit-identical to
+    content_mvn_loss + style_loss_weighted with autograd adding their gradients."""
+    x = rnd(81, shape, 1.1, 0.3).to(hip_device)
+    yc = rnd(82, shape, 0.8, 0.4).to(hip_device)
+    ys = rnd(83, shape, 1.4, 0.1).to(hip_device)
+    xa = x.clone().requires_grad_()
+    c, s = L.content_style_loss(xa, yc, ys, 0.3, 0.75)
+    (2.0 * c + 0.5 * s).backward()
+    xb = x.clone().requires_grad_()
+    c2, s2 = L.content_mvn_loss(xb, yc, 0.3), L.style_loss_weighted(xb, ys, 0.75)
+    (2.0 * c2 + 0.5 * s2).backward()
+    assert torch.equal(c, c2) and torch.equal(s, s2)
+    assert torch.equal(xa.grad, xb.grad)
+
+
 @pytest.mark.parametrize("canonical,alpha,style_hw", [(False, 1.0, (6, 6)), (True, 0.6, (6, 6)), (False, 0.3, (9, 5))])
 def test_adain_backward(canonical, alpha, style_hw, hip_device):
     c = rnd(61, (2, 8, 6, 6), 2.0, 0.5)
