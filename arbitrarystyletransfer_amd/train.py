@@ -327,8 +327,16 @@ class ASTTrainer:
                 content_map, style_map = self.pretrained_enc(content), self.pretrained_enc(style)
             # :198 (the reference records autograd here but only ever uses the result detached)
             enc_stylized = self.ast._enc(stylized.detach(), out_layers=enc_out_layers)
-        t_cs_map = self.pretrained_enc(stylized)                                        # :195
-        org_out_map = self.pretrained_enc(org_out)                                      # :196
+        if stylized.shape == org_out.shape:
+            # :195-196 in ONE pass over both batches: the loss network's small maps (20^2, 10^2 at
+            # 512 channels) fill twice the workgroups per launch; every conv is per image, so each
+            # half equals its own pass (the frozen network has no weight gradient to mix them)
+            both_maps = self.pretrained_enc(torch.cat([stylized, org_out]))
+            halves = [m.split(b) for m in both_maps]
+            t_cs_map, org_out_map = [h[0] for h in halves], [h[1] for h in halves]
+        else:
+            t_cs_map = self.pretrained_enc(stylized)                                    # :195
+            org_out_map = self.pretrained_enc(org_out)                                  # :196
         # :217-227 content and :230-245 style terms per tap, :258 / :271 on the image, pairwise fused
         pairs = [L.content_style_loss(x, yc, ys, 1.0, w) for x, yc, ys, w in zip(t_cs_map, content_map, style_map,
                                                                                 STYLE_WEIGHTS)]
