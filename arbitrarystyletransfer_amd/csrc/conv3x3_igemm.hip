@@ -988,14 +988,13 @@ __global__ __launch_bounds__(256, 3) void conv3x3_smallc_kernel(ConvArgs a) {
         float v[NV];
         if constexpr (UP == 1) {
           // columns 4tx-1 .. 4tx+4: one aligned 16-byte read (consecutive lanes, conflict-free) and
-          // the two neighbours from the adjacent lanes (DPP wave shifts); the scalar reads at a
+          // the two neighbours from the adjacent lanes (lane shuffles); the scalar reads at a
           // 4-word lane stride were 4-way bank conflicts. Each half-wave is one output row, so its
           // first and last lanes read their outer neighbour themselves.
           const float4 mid = *reinterpret_cast<const float4*>(rowp + 4 * tx);
-          float left = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, mid.w), 0x138,
-                                                                           0xf, 0xf, false));  // wave_shr:1
-          float right = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, mid.x), 0x130,
-                                                                            0xf, 0xf, false));  // wave_shl:1
+          // (lane shuffles; the DPP wave_shr / wave_shl forms these replaced are GFX8/9-era controls)
+          float left = __shfl_up(mid.w, 1, 64);
+          float right = __shfl_down(mid.x, 1, 64);
           if (tx == 0) left = rowp[-1];
           if (tx == 31) right = rowp[128];
           v[0] = left;
@@ -1060,6 +1059,11 @@ __global__ __launch_bounds__(256, 3) void conv3x3_smallc_kernel(ConvArgs a) {
 // the workgroup's weights sit in LDS and each tap's 4 output channels are one broadcast 16-byte
 // read (as wave-uniform scalar loads, 108 weights per trip spilled 150 SGPRs: 2 SGPR reloads per
 // FMA pair); every store is a 512-B row run.
+// NTS (configs 20, 22, 23) used to store through nontemporal stores; it is kept only as a
+// configuration index and stores normally: the nontemporal form was the first suspect for the
+// run-to-run differences seen under a second process's GPU load (DESIGN.md §4 open item), and the
+// plain form costs nothing measurable (config 2: 568.6 img/s, profiles/r03_race_fix_trials.txt) --
+// but the differences persist without it, so it was not their cause.
 template <int CIN, bool NORM, int TH, bool NTS, int OCC>
 __global__ __launch_bounds__(TH * 32, OCC) void conv3x3_cin4_kernel(ConvArgs a, const float* __restrict__ wp) {
   constexpr int NT = TH * 32, TWS = 128, COG = 4;
@@ -1166,16 +1170,14 @@ __global__ __launch_bounds__(TH * 32, OCC) void conv3x3_cin4_kernel(ConvArgs a, 
       const int64_t off = obase + (int64_t)co * plane;
       if (a.y_pre) {
         if (full) {
-          if (NTS) __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4*>(a.y_pre + off));
-          else *reinterpret_cast<float4*>(a.y_pre + off) = make_float4(o[0], o[1], o[2], o[3]);
+          *reinterpret_cast<float4*>(a.y_pre + off) = make_float4(o[0], o[1], o[2], o[3]);
         } else {
           for (int j = 0; j < 4; ++j) if (xx + j < W) a.y_pre[off + j] = o[j];
         }
       }
       if (a.y_act) {
         if (full) {
-          if (NTS) __builtin_nontemporal_store(f32x4{u[0], u[1], u[2], u[3]}, reinterpret_cast<f32x4*>(a.y_act + off));
-          else *reinterpret_cast<float4*>(a.y_act + off) = make_float4(u[0], u[1], u[2], u[3]);
+          *reinterpret_cast<float4*>(a.y_act + off) = make_float4(u[0], u[1], u[2], u[3]);
         } else {
           for (int j = 0; j < 4; ++j) if (xx + j < W) a.y_act[off + j] = u[j];
         }
