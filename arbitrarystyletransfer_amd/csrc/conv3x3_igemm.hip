@@ -1254,7 +1254,11 @@ int launch_cin4(const ConvArgs& a0, hipStream_t s, int up) {
   if (nblk >= 0x7fffffff) return AST_E_SHAPE;
   const dim3 g((unsigned)nblk), b(TH * 32);
   const bool norm = a.in_mean != nullptr;
-  const size_t wl = (size_t)a.Cin * 9 * a.cout_pad * sizeof(float);  // weights in LDS
+  // weights in LDS: the instantiation's CIN (3, else 4: Cin 1 and 2 run the CIN = 4 kernel, which
+  // copies and reads 4 channels' slabs -- the packed fp32 part holds cin_pad8 >= 4 of them, zero past
+  // Cin), not a.Cin, or channels Cin..3 are read past the allocation
+  const int cin_k = a.Cin == 3 ? 3 : 4;
+  const size_t wl = (size_t)cin_k * 9 * a.cout_pad * sizeof(float);
   if (a.cout_pad % 4 || wl > 32 * 1024) return AST_E_UNSUPPORTED;
   if (a.Cin == 3) {
     if (norm) hipLaunchKernelGGL((conv3x3_cin4_kernel<3, true, TH, NTS, OCC>), g, b, wl, s, a, a.wp);

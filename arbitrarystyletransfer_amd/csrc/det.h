@@ -49,6 +49,10 @@ __device__ __forceinline__ void loss_acc_commit(float* acc, float v) {
   }
   __syncthreads();
   if (!last_) return;
+  // Every reading thread acquires at agent scope, not only thread 0 (whose fetch_add did): the
+  // partials come from workgroups on other XCDs, whose L2s are not coherent with this one's, and the
+  // workgroup barrier alone orders nothing beyond the workgroup.
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   float s = 0.f;
   for (unsigned i = threadIdx.x; i < nb; i += blockDim.x)
     s += __hip_atomic_load(acc + 2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

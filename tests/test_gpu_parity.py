@@ -62,6 +62,10 @@ CONV_CASES = [
     (1, 3, 9, 130, 16, 1, "reflect", False),  # cin 3, cout 16 (MobileNet block 0 class), W % 4 != 0, 2 x-tiles
     (2, 4, 12, 64, 24, 1, "zeros", False),   # cin 4, cout 24
     (1, 1, 5, 36, 64, 1, "reflect", False),   # cin 1 (zero channels of the 4-channel template)
+    # cin 1 / 2 on the direct kernel with wide weight slabs: its LDS holds the CIN = 4 template's
+    # 4 x 9 x cout_pad weights (sized by Cin before round 4, which read past the allocation)
+    (1, 2, 10, 70, 128, 1, "zeros", False),
+    (2, 1, 9, 128, 192, 1, "reflect", False),
     (2, 3, 16, 256, 64, 1, "zeros", True),    # conv_1: full 128-px tiles, normalised gather
     (1, 18, 8, 256, 3, 1, "reflect", False),  # cout 3, vector-staged tiles, partial last K chunk
     (1, 10, 6, 128, 4, 2, "reflect", False),  # cout 4, upsampled, vector-staged tiles
@@ -94,6 +98,22 @@ def test_conv3x3_all_configs(case, hip_device):
         if pool_r is not None:
             assert rel_inf(pool, pool_r) <= OP_TOL, cfg
     assert tried >= 1
+
+
+@pytest.mark.parametrize("cin", [1, 2, 3, 4])
+def test_conv3x3_direct_cin_le4_lds_weights(cin, hip_device):
+    """The direct cin <= 4 kernel (configs 18-23) on every cin it takes, with a 192-channel weight
+    slab (27.6 KB of LDS for the 4-channel template): launched explicitly, never rejected."""
+    x = torch.from_numpy(synth.image(40 + cin, (2, cin, 12, 136)) * 2 - 0.5)
+    wt = torch.from_numpy(synth.conv_weight(50 + cin, 192, cin, 3))
+    bs = torch.from_numpy(synth.conv_bias(60 + cin, 192))
+    pre_r, act_r, _ = oracle_conv(x, wt, bs, 1, "reflect", False, True)
+    xd, wp, bd = x.to(hip_device), ops.pack_conv3x3(wt.to(hip_device)), bs.to(hip_device)
+    for cfg in range(18, 24):
+        pre, act, _ = ops.conv3x3(xd, wp, bd, 192, pad_mode="reflect", want_pre=True, want_act=True, cfg=cfg)
+        torch.cuda.synchronize()
+        assert rel_inf(pre, pre_r) <= OP_TOL, (cin, cfg, rel_inf(pre, pre_r))
+        assert rel_inf(act, act_r) <= OP_TOL, (cin, cfg)
 
 
 def test_conv3x3_pair_input_matches_concat(hip_device):
