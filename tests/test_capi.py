@@ -119,3 +119,42 @@ def test_torch_ops_registered_with_meta_kernels():
         o.conv3x3_fwd(x, pk, None, 128, 1, 0, None, None, True, False, False, -1)
     with pytest.raises(NotImplementedError):   # no CPU kernel: there is no CPU fallback
         o.adain(torch.zeros(1, 2, 3, 3), torch.zeros(1, 2, 3, 3), 1.0, True)
+
+
+def _gfx950_code_objects(path):
+    """The gfx950 code objects of the clang offload bundles embedded in a host library."""
+    import struct
+    data = open(path, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    out = []
+    i = data.find(magic)
+    while i != -1:
+        num = struct.unpack_from("<Q", data, i + 24)[0]
+        off = i + 32
+        for _ in range(num):
+            o, sz, idl = struct.unpack_from("<QQQ", data, off)
+            tid = data[off + 24:off + 24 + idl].decode()
+            off += 24 + idl
+            if "gfx950" in tid:
+                out.append(data[i + o:i + o + sz])
+        i = data.find(magic, i + 1)
+    return out
+
+
+def test_no_packed_fp32_valu_in_kernels(tmp_path):
+    """No kernel of libast_hip.so contains a packed-FP32 VALU instruction (v_pk_fma/mul/add_f32): with
+    another process's waves on the same CUs they dropped results in lanes 48-55 (DESIGN.md §4,
+    profiles/r04_race_diffmap.txt), so the library is built without the packed-fp32-ops feature."""
+    import subprocess
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not available")
+    cos = _gfx950_code_objects(_lib.LIB_PATH)
+    assert len(cos) >= 10
+    for k, co in enumerate(cos):
+        f = tmp_path / f"co{k}.elf"
+        f.write_bytes(co)
+        dis = subprocess.run([objdump, "-d", str(f)], capture_output=True, text=True, check=True).stdout
+        assert "s_endpgm" in dis
+        bad = [ln.strip() for ln in dis.splitlines() if re.search(r"\bv_pk_(fma|mul|add)_f32\b", ln)]
+        assert not bad, (k, bad[:4])
