@@ -149,3 +149,129 @@ def test_syncbn_stats_gather_and_merge(tmp_path):
     np.testing.assert_allclose(var, xn.var(axis=(0, 2, 3)), rtol=1e-10)
     assert (cnt == 5 * 7 * 6).all()
     assert torch.equal(r0["sums"], torch.tensor([[3.0] * 3, [6.0] * 3])) and torch.equal(r0["sums"], r1["sums"])
+
+
+def _world8_worker(rank, world, port, content, style, result_path):
+    """BASELINE.json config 4's data-parallel step at world size 8 (gloo): AdaINTrainer's semantics
+    (arbitrarystyletransfer_amd/train.py:202-215) with the oracle's losses — each rank weights its
+    batch-mean terms by local/global (the sum-type TV term is additive), backward, the flat arena's
+    SUM all-reduce, clip_grad_norm_(2.0) + Adam (train.py:287-300). Also the one-style broadcast and
+    an 8-part SyncBatchNorm gather + merge."""
+    from oracle import ref_cpu as R
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    gb = content.shape[0]
+    a, b = dp.shard_range(gb, rank, world)
+    w = dp.shard_weight(gb, rank, world)
+    enc = [(torch.from_numpy(x), torch.from_numpy(y)) for x, y in synth.vgg_encoder_weights(1)]
+    dec = [(torch.from_numpy(x).clone().requires_grad_(), torch.from_numpy(y).clone().requires_grad_())
+           for x, y in synth.vgg_decoder_weights(2)]
+    params = [p for wb in dec for p in wb]
+    out = R.train_losses(content[a:b], style[a:b], enc, dec)
+    (w * (1.25 * out["content_loss"] + 0.5 * out["style_loss"] + 1.0 * out["lf_loss"])
+     + 0.0006 * out["tv_loss"]).backward()
+    arena = dp.FlatGradArena(params, device=torch.device("cpu"), average=False)
+    try:
+        arena.all_reduce()
+    finally:
+        arena.unregister()
+    grads = [p.grad.detach().clone() for p in params]
+    opt = torch.optim.Adam(params, lr=2e-4, betas=[0.9, 0.999], eps=1e-5)
+    norm = torch.nn.utils.clip_grad_norm_(params, 2.0, error_if_nonfinite=True)
+    opt.step()
+    # one style image owned by rank 0, broadcast to every rank
+    with torch.no_grad():
+        if rank == 0:
+            m, s = R.channel_stats(R.vgg_encoder(style[:1], enc[:9])[0])
+            m, s = m.flatten(), s.flatten()
+        else:
+            m, s = torch.zeros(512), torch.full((512,), float("nan"))
+        m, s = dp.broadcast_style_stats(m, s, src=0)
+    # SyncBatchNorm statistics of an 8-way sharded activation
+    act = content[:, :, :5, :7] * 3 + 1
+    allst = dp.all_gather_bn_stats(torch.from_numpy(R.bn_shard_stats(act[a:b].numpy())))
+    torch.save({"grads": grads, "params": [p.detach().clone() for p in params], "norm": float(norm),
+                "m": m, "s": s, "allst": allst}, result_path + f".{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _shard_grads(content, style, a, b, w, dtype):
+    """Decoder gradients of AdaINTrainer's rank-local objective on images a..b (shard weight w)."""
+    from oracle import ref_cpu as R
+    enc = [(torch.from_numpy(x).to(dtype), torch.from_numpy(y).to(dtype)) for x, y in synth.vgg_encoder_weights(1)]
+    dec = [(torch.from_numpy(x).to(dtype).requires_grad_(), torch.from_numpy(y).to(dtype).requires_grad_())
+           for x, y in synth.vgg_decoder_weights(2)]
+    out = R.train_losses(content[a:b].to(dtype), style[a:b].to(dtype), enc, dec)
+    (w * (1.25 * out["content_loss"] + 0.5 * out["style_loss"] + 1.0 * out["lf_loss"])
+     + 0.0006 * out["tv_loss"]).backward()
+    return [p.grad for wb in dec for p in wb]
+
+
+def test_dp_world8_step_matches_single_process(tmp_path):
+    """Config 4 readiness without an 8-GPU node: 8 gloo ranks, a global batch
+    of 13 (uneven shards 2,2,2,2,2,1,1,1). (1) The semantics, in float64: the shard-weighted rank
+    objectives sum to exactly the single-process full-batch gradient. (2) The plumbing, in fp32: the
+    arena's SUM all-reduce equals the rank gradients summed here, every rank holds the same reduced
+    gradient, gradient norm and post-clip + Adam weights (equal to torch's clip + Adam on that sum),
+    the same broadcast style statistics, and the same 8-part BatchNorm statistics, whose merge equals
+    the whole batch's. (fp32 is not compared with the full-batch step itself: the oracle's fp32
+    evaluation moves by ~1e-2 relative between batch sizes through the 2x2 mean-variance-norm taps,
+    while float64 agrees to 1e-13.)"""
+    from oracle import ref_cpu as R
+    gb, world = 13, 8
+    spans = [dp.shard_range(gb, r, world) for r in range(world)]
+    assert [b - a for a, b in spans] == [2, 2, 2, 2, 2, 1, 1, 1]
+    content = torch.from_numpy(synth.image(951, (gb, 3, 32, 32)))
+    style = torch.from_numpy(synth.image(952, (gb, 3, 32, 32)))
+    # (1) semantics
+    full = _shard_grads(content, style, 0, gb, 1.0, torch.float64)
+    parts = [_shard_grads(content, style, a, b, dp.shard_weight(gb, r, world), torch.float64)
+             for r, (a, b) in enumerate(spans)]
+    for i, g in enumerate(full):
+        s = sum(p[i] for p in parts)
+        assert float((s - g).abs().max()) <= 1e-10 * float(g.abs().max()), i
+    # (2) plumbing
+    path = str(tmp_path / "w8")
+    mp.spawn(_world8_worker, args=(world, _free_port(), content, style, path), nprocs=world, join=True)
+    res = [torch.load(path + f".{r}", weights_only=True) for r in range(world)]
+    for r in range(world):
+        for g0, g in zip(res[0]["grads"], res[r]["grads"]):
+            assert torch.equal(g0, g)
+        for p0, p in zip(res[0]["params"], res[r]["params"]):
+            assert torch.equal(p0, p)
+        assert torch.equal(res[r]["m"], res[0]["m"]) and torch.equal(res[r]["s"], res[0]["s"])
+        assert torch.equal(res[r]["allst"], res[0]["allst"])
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)   # as the ranks: the oracle's fp32 gradients depend on the CPU kernels' split
+    try:
+        parts32 = [_shard_grads(content, style, a, b, dp.shard_weight(gb, r, world), torch.float32)
+                   for r, (a, b) in enumerate(spans)]
+    finally:
+        torch.set_num_threads(nt)
+    ref = [sum(p[i] for p in parts32) for i in range(len(parts32[0]))]
+    for g, gr in zip(res[0]["grads"], ref):   # the collective's summation order only
+        np.testing.assert_allclose(g.numpy(), gr.numpy(), rtol=1e-5, atol=1e-6 * float(gr.abs().max()))
+    params = [torch.nn.Parameter(torch.from_numpy(x).clone()) for wb in synth.vgg_decoder_weights(2) for x in wb]
+    for p, g in zip(params, ref):
+        p.grad = g.clone()
+    opt = torch.optim.Adam(params, lr=2e-4, betas=[0.9, 0.999], eps=1e-5)
+    norm = torch.nn.utils.clip_grad_norm_(params, 2.0, error_if_nonfinite=True)
+    opt.step()
+    np.testing.assert_allclose(res[0]["norm"], float(norm), rtol=1e-5)
+    for p, pr in zip(res[0]["params"], params):
+        diff = (p - pr.detach()).abs()
+        # Adam's first step is ~lr*sign(g): elements whose gradient is within rounding of 0 may differ
+        assert float((diff > 1e-6).float().mean()) <= 1e-3 and float(diff.max()) <= 4e-4
+    enc = [(torch.from_numpy(x), torch.from_numpy(y)) for x, y in synth.vgg_encoder_weights(1)]
+    with torch.no_grad():
+        m, s = R.channel_stats(R.vgg_encoder(style[:1], enc[:9])[0])
+    np.testing.assert_allclose(res[0]["m"].numpy(), m.flatten().numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(res[0]["s"].numpy(), s.flatten().numpy(), rtol=1e-5, atol=1e-6)
+    assert res[0]["allst"].shape == (world, 3, 3)
+    mu, var, cnt = R.bn_merge_stats(res[0]["allst"].numpy())
+    act = (content[:, :, :5, :7] * 3 + 1).numpy().astype(np.float64)
+    np.testing.assert_allclose(mu, act.mean(axis=(0, 2, 3)), rtol=1e-10)
+    np.testing.assert_allclose(var, act.var(axis=(0, 2, 3)), rtol=1e-9)
+    assert (cnt == gb * 5 * 7).all()

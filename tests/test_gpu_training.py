@@ -526,13 +526,16 @@ def test_full_losses_step_with_grad_arena(hip_device):
         assert np.mean(diff > 1e-6) <= 1e-3 and diff.max() <= 4e-4
 
 
-@pytest.mark.parametrize("global_batch,full", [(3, False), (2, True)])
-def test_adain_dp_two_ranks_match_single_process(global_batch, full, tmp_path, hip_device):
+@pytest.mark.parametrize("global_batch,full,nproc", [(3, False, 2), (2, True, 2), (61, False, 8)])
+def test_adain_dp_ranks_match_single_process(global_batch, full, nproc, tmp_path, hip_device):
     """BASELINE.json config 4 on the HIP path: two ranks
     (torch.distributed.run, gloo on the one GPU) each run AdaINTrainer on their shard of the global
     batch (3 images: uneven 2 + 1 shards; 2 images with the full train.py loss), the decoder
     gradients meet in dp.FlatGradArena's one all-reduce, then clip + Adam. The reduced gradient and
-    the updated weights must equal one process stepping the whole batch (train.py:287-300)."""
+    the updated weights must equal one process stepping the whole batch (train.py:287-300).
+    nproc 8: config 4's world size, 8 ranks on the one GPU, global batch 61 in
+    uneven shards 8,8,8,8,8,7,7,7 (config 4 itself is 64 = 8 x 8 at 512^2, one rank per GPU over
+    RCCL: the driver's multi-GPU run)."""
     import os
     import socket
     import subprocess
@@ -544,7 +547,7 @@ def test_adain_dp_two_ranks_match_single_process(global_batch, full, tmp_path, h
     size = 64
     out = str(tmp_path / "dp.npz")
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "adain_dp_worker.py")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                         "--master-addr=127.0.0.1", f"--master-port={port}", worker, out, str(global_batch), str(size)]
                        + (["full"] if full else []), capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
