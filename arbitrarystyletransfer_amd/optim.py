@@ -184,6 +184,11 @@ class FusedAdam(torch.optim.Optimizer):
             assert t.build([p.data for p in allp], [p.grad for p in allp], None, None, dev) == nchunks
         torch.cuda.current_stream(dev).synchronize()   # the pinned tables have reached the device
 
+    def static_hyper(self):
+        """The hyper-parameters step_static bakes into its launches (StepGraph recaptures on change)."""
+        return (tuple((float(g["lr"]), tuple(float(b) for b in g["betas"]), float(g["eps"])) for g in self.param_groups),
+                self.max_grad_norm, self.error_if_nonfinite)
+
     def step_static(self):
         """clip_grad_norm_ + Adam on the static tables, capturable: a non-finite norm skips the
         update on the device (the caller checks last_grad_norm after the replay and raises)."""

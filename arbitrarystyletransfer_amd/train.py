@@ -57,7 +57,12 @@ class StepGraph:
         self.optim, self.arena, self.params, self.body = optim, arena, list(params), body
         self.frozen = list(frozen)   # frozen networks whose weight packs are built once, outside the graph
         self.graph = None
-        self.shapes = None
+        self.key = None   # (input shapes, optimizer hyper-parameters) the graph was captured for
+
+    def _key(self, inputs):
+        # the captured clip + Adam launches carry lr, betas, eps and max_grad_norm as kernel
+        # arguments: a change (a scheduler, load() resetting the lr, train.py:94-98) recaptures
+        return ([tuple(x.shape) for x in inputs], self.optim.static_hyper())
 
     def _capture(self, inputs):
         for net in self.frozen:
@@ -76,10 +81,13 @@ class StepGraph:
             self.out = self.body(*self.static)
         self.optim.fill_static()
         self.graph = g
-        self.shapes = [tuple(x.shape) for x in inputs]
+        self.key = self._key(inputs)
 
     def run(self, *inputs):
-        if self.graph is None or self.shapes != [tuple(x.shape) for x in inputs]:
+        """One replayed step. The returned tensors are copies: the next replay overwrites the
+        captured step's own outputs in place, so a caller keeping a step's results (to log or show
+        them later) gets what eager mode gives."""
+        if self.graph is None or self.key != self._key(inputs):
             self._capture(inputs)
         for s_, x in zip(self.static, inputs):
             s_.copy_(x)
@@ -91,9 +99,17 @@ class StepGraph:
                                    "so it cannot be clipped (error_if_nonfinite=True, train.py:292); the step was "
                                    "not applied")
         self.optim.after_static_step()
-        out = dict(self.out)
-        out["grad_norm"] = self.optim.last_grad_norm
+        out = {k: _detached_copy(v) for k, v in self.out.items()}
+        out["grad_norm"] = self.optim.last_grad_norm.clone()
         return out
+
+
+def _detached_copy(v):
+    if isinstance(v, torch.Tensor):
+        return v.detach().clone()
+    if isinstance(v, (list, tuple)):
+        return type(v)(_detached_copy(x) for x in v)
+    return v
 
 
 STYLE_WEIGHTS = (1.0, 1.0, 1.0, 1.0, 0.75, 0.5)   # train.py:232-238 for the 6 loss-network layers
@@ -291,9 +307,17 @@ class ASTTrainer:
             dp.shard_range(self.args.batch_size, self.rank, self.world)
             dp.convert_sync_batchnorm(self.ast)
             self.grad_arena = dp.FlatGradArena(self.params, average=False)
-        # graph mode (default on: the step is launch-bound at the reference's 160^2 training size):
-        # the whole step replays as one hipGraph (StepGraph); grad_hook is then not called
-        self.graph = (getattr(self.args, "graph", True) if graph is None else graph) and grad_hook is None
+        # graph mode (default on in one process: the step is launch-bound at the reference's 160^2
+        # training size): the whole step replays as one hipGraph (StepGraph); grad_hook is then not
+        # called. Off by default under data parallelism: gloo stages every collective through the
+        # host (a synchronising copy, which a capture refuses), and capturing the RCCL all-reduce
+        # and SyncBatchNorm's all-gather at world size > 1 has not been verified.
+        if graph is None:
+            graph = getattr(self.args, "graph", self.world == 1)
+        if graph and self.world > 1 and dist.get_backend() != "nccl":
+            raise ValueError("ASTTrainer(graph=True) needs the nccl (RCCL) backend under data parallelism: "
+                             "gloo collectives stage through the host and cannot be captured")
+        self.graph = graph and grad_hook is None
         self._step_graph = None
         if self.graph:
             if self.grad_arena is None:   # persistent gradient storage for the captured optimizer tables

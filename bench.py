@@ -195,7 +195,8 @@ def ast_train_bench(args, dev, rank, world):
     all-reduce."""
     from arbitrarystyletransfer_amd.train import ASTTrainer, default_ast_args
     B, S = args.batch or 8, args.size or 160
-    graph = os.environ.get("AST_TRAIN_GRAPH", "1") != "0"
+    # hipGraph replay in one process; eager under data parallelism (ASTTrainer's default there)
+    graph = os.environ.get("AST_TRAIN_GRAPH", "1" if world == 1 else "0") != "0"
     trainer = ASTTrainer(default_ast_args(batch_size=B * world), device=dev,
                          ast=models.AST(attention=True).load_live_init(), graph=graph)
     content = torch.from_numpy(synth.image(905 + rank, (B, 3, S, S))).to(dev)

@@ -215,8 +215,10 @@ def test_ast_trainer_dp_uneven_matches_single_process(tmp_path, hip_device):
 def test_ast_trainer_graph_matches_eager(hip_device):
     """ASTTrainer's hipGraph mode (train.StepGraph: the whole step -- forward, backward, gradient
     arena, clip + Adam with the step count on the device -- replayed as one graph) against the
-    eager step: two steps from the same initial state give the same losses, gradient norms and
-    parameters (bitwise: the same kernels run in the same order; the Adam bias corrections are
+    eager step: two steps from the same initial state, the lr changed between them (the graph is
+    recaptured), give the same losses, gradient norms and parameters, and a step's returned outputs
+    are not overwritten by the next replay (bitwise: the same kernels run in the same order; the Adam
+    bias corrections are
     computed on the device in double, as the host does, allowed one fp32 ulp). A non-finite
     gradient norm raises after the replay and leaves every parameter unchanged."""
     from arbitrarystyletransfer_amd.train import ASTTrainer, default_ast_args
@@ -229,9 +231,16 @@ def test_ast_trainer_graph_matches_eager(hip_device):
                         ast=models.AST(attention=True).load_live_init(), graph=graph)
         assert tr.graph == graph
         vals = []
-        for _ in range(2):   # graph mode: the outputs are the captured step's static tensors, read them now
+        for i in range(2):
+            if i == 1:   # a changed lr (a scheduler, load(): train.py:94-98) must reach the replayed step
+                for g in tr.ast_optim.param_groups:
+                    g["lr"] = 1e-4
             o = tr.train_step(c, s, record=True)
+            if i == 0:
+                o0, keep = o, o["stylized"].clone()
             vals.append((float(o["loss"]), float(o["grad_norm"])))
+        # a step's outputs are the caller's: the next replay does not overwrite them (advisor r3)
+        assert torch.equal(o0["stylized"], keep)
         runs[graph] = (tr, vals,
                        [p.detach().clone() for p in tr.params], dict(tr.train_dict))
     (te, le, pe, de), (tg, lg, pg, dg) = runs[False], runs[True]
