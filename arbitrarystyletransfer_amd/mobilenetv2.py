@@ -7,11 +7,12 @@ unchanged; the forwards run on the fused kernels of csrc/mobilenet.hip (C ABI `a
     conv_3x3_bn    (mobilenetv2.py:38-43)   ast_mb_conv3x3_dense
     SELayer        (mobilenetv2.py:63-81)   fused into DepthWiseConv (pool sums + gate folding)
 
-Scope: inference. BatchNorm runs with its running statistics (eval mode)
-and is folded into the conv weights; calling a block with BatchNorm in training mode, or with
-autograd recording, raises instead of silently diverging from the reference. Activations are
-stored in the parameters' dtype (float32, or bfloat16 after `.to(torch.bfloat16)`); arithmetic
-and accumulation are fp32.
+Eval mode (the inference path): BatchNorm runs with its running statistics and
+is folded into the conv weights. Training mode or autograd recording (train_autoencoder.py,
+train.py's ASTTrainer) dispatches to the composable training kernels of mbtrain.py
+(csrc/mbtrain.hip: batch statistics, running-stat updates, every intermediate kept for backward).
+Activations are stored in the parameters' dtype (float32, or bfloat16 after
+`.to(torch.bfloat16)`); arithmetic and accumulation are fp32.
 """
 from __future__ import annotations
 
