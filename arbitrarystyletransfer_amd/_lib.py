@@ -80,6 +80,10 @@ SIGNATURES = {
     "ast_adaattn_dv_f32": (_i, [_p, _p, _p, _i, _ll, _p]),
     "ast_instance_norm_backward_f32": (_i, [_p, _p, _p, _p, _p, _ll, _ll, _i, _p]),
     "ast_fma_inplace_f32": (_i, [_p, _p, _p, _ll, _p]),
+    "ast_adaattn_flash_supported": (_i, [_i]),
+    "ast_adaattn_flash_stats_f32": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),
+    "ast_adaattn_flash_bwd_kv_f32": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),
+    "ast_adaattn_flash_bwd_q_f32": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),
     "ast_adaattn_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i, _i, _i, _i]),
     "ast_adaattn_fwd": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, ctypes.c_size_t, _i, _i, _i, _i, _i, _i, _p]),
     "ast_soft_hist_workspace_floats": (_ll, [_i]),

@@ -5,10 +5,17 @@ Forward: ops.adaattn (one fused flash-style launch; the Nq x Nk attention matrix
 registers). Backward: the attention is recomputed per image with the batched MFMA GEMMs of
 csrc/mbtrain.hip (`ast_mbt_gemm_f32`, strided operands, fp32 as the reference trains) and the
 elementwise / row-reduction stages of csrc/adaattn_bwd.hip; the derivation is in that file's head.
-Here P is materialised: [n][Nq][Nk] fp32 is 64 MB at the trainer's 256^2 images (32^2 maps, B=16)
-and 1 GB at 512^2 -- well inside 288 GB of HBM, and the GEMMs then run at full tile width.
+Two forms of the attention part of the backward:
+  * materialised (small maps): P and dS as [n][Nq][Nk] fp32 through the batched GEMMs -- 5 MB at the
+    reference's 160^2 training images (20^2 maps, B=8), where full-width GEMM tiles win;
+  * flash (csrc/adaattn_flash.hip; round 4), once P would reach FLASH_MIN_BYTES (64 MiB: 64^2 maps
+    at one image): the scores are recomputed per 16 x 16 block in registers by three passes (row
+    statistics; dK and d[V; V^2] per key; dQ per query) and neither P nor dS is ever stored -- they
+    grow as (H W)^2, 1 GB per image at 128^2 maps. AST_ADAATTN_FLASH=1|0 forces one form.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -25,6 +32,17 @@ def _in_stats(x):
     """InstanceNorm2d (models.py:77-79: affine=False, eps 1e-5, biased variance): mean, std, x_hat."""
     m, s = ops.channel_stats(x, unbiased=False, eps=1e-5)
     return m, s, ops.plane_normalize(x, m, s)
+
+
+FLASH_MIN_BYTES = 64 << 20
+
+
+def use_flash(n, C, N, M) -> bool:
+    """Whether AdaAttNFn.backward takes the flash form (see the module docstring)."""
+    env = os.environ.get("AST_ADAATTN_FLASH")
+    if env == "0" or not lib().ast_adaattn_flash_supported(int(C)):
+        return False
+    return env == "1" or 4 * n * N * M >= FLASH_MIN_BYTES
 
 
 def _wsplit(n, k):
@@ -62,26 +80,39 @@ class AdaAttNFn(torch.autograd.Function):
         gemm(Wk, shat, K, C, M, C, n, (0, C, 1), (C * M, M, 1), (C * M, M, 1), role="attn k")
         gemm(Wv, s, VV, C, M, C, n, (0, C, 1), (C * M, M, 1), (2 * C * M, M, 1), role="attn v")
         check(L.ast_adaattn_square_f32(ptr(VV), n, C * M, st), "adaattn_square")
-        P = f(n, N, M)
-        gemm(Q, K, P, N, M, C, n, (C * N, 1, N), (C * M, M, 1), (N * M, M, 1), role="attn s")
-        check(L.ast_softmax_rows_f32(ptr(P), n * N, M, st), "softmax_rows")
+        flash = use_flash(n, C, N, M)
         O2 = f(n, N, 2 * C)
-        gemm(P, VV, O2, N, 2 * C, M, n, (N * M, M, 1), (2 * C * M, 1, M), (N * 2 * C, 2 * C, 1), role="attn o")
+        if flash:
+            lse2 = f(n, N)
+            check(L.ast_adaattn_flash_stats_f32(ptr(Q), ptr(K), ptr(VV), ptr(O2), ptr(lse2), n, C, N, M, st),
+                  "adaattn_flash_stats")
+        else:
+            P = f(n, N, M)
+            gemm(Q, K, P, N, M, C, n, (C * N, 1, N), (C * M, M, 1), (N * M, M, 1), role="attn s")
+            check(L.ast_softmax_rows_f32(ptr(P), n * N, M, st), "softmax_rows")
+            gemm(P, VV, O2, N, 2 * C, M, n, (N * M, M, 1), (2 * C * M, 1, M), (N * 2 * C, 2 * C, 1), role="attn o")
         dO2, D = f(n, N, 2 * C), f(n * N)
         need_dc = ctx.needs_input_grad[0]
         std = f(n, C, N) if need_dc else None
         check(L.ast_adaattn_dstats_f32(ptr(O2), ptr(g), ptr(chat), ptr(dO2), ptr(D), ptr(std), n, C, N, st),
               "adaattn_dstats")
-        dS = f(n, N, M)
-        gemm(dO2, VV, dS, N, M, 2 * C, n, (N * 2 * C, 2 * C, 1), (2 * C * M, M, 1), (N * M, M, 1), role="attn dp")
-        check(L.ast_softmax_backward_f32(ptr(P), ptr(dS), ptr(D), n * N, M, st), "softmax_backward")
         dVV = f(n, 2 * C, M)
-        gemm(dO2, P, dVV, 2 * C, M, N, n, (N * 2 * C, 1, 2 * C), (N * M, M, 1), (2 * C * M, M, 1), role="attn dvv")
+        dQ, dK = f(n, C, N), f(n, C, M)
+        if flash:
+            check(L.ast_adaattn_flash_bwd_kv_f32(ptr(Q), ptr(K), ptr(VV), ptr(dO2), ptr(lse2), ptr(D), ptr(dK),
+                                                 ptr(dVV), n, C, N, M, st), "adaattn_flash_bwd_kv")
+            check(L.ast_adaattn_flash_bwd_q_f32(ptr(Q), ptr(K), ptr(VV), ptr(dO2), ptr(lse2), ptr(D), ptr(dQ),
+                                                n, C, N, M, st), "adaattn_flash_bwd_q")
+        else:
+            dS = f(n, N, M)
+            gemm(dO2, VV, dS, N, M, 2 * C, n, (N * 2 * C, 2 * C, 1), (2 * C * M, M, 1), (N * M, M, 1), role="attn dp")
+            check(L.ast_softmax_backward_f32(ptr(P), ptr(dS), ptr(D), n * N, M, st), "softmax_backward")
+            gemm(dO2, P, dVV, 2 * C, M, N, n, (N * 2 * C, 1, 2 * C), (N * M, M, 1), (2 * C * M, M, 1), role="attn dvv")
+            gemm(K, dS, dQ, C, N, M, n, (C * M, M, 1), (N * M, 1, M), (C * N, N, 1), role="attn dq")
+            gemm(Q, dS, dK, C, M, N, n, (C * N, N, 1), (N * M, M, 1), (C * M, M, 1), role="attn dk")
+            del P, dS
         dV = f(n, C, M)
         check(L.ast_adaattn_dv_f32(ptr(dVV), ptr(VV), ptr(dV), n, C * M, st), "adaattn_dv")
-        dQ, dK = f(n, C, N), f(n, C, M)
-        gemm(K, dS, dQ, C, N, M, n, (C * M, M, 1), (N * M, 1, M), (C * N, N, 1), role="attn dq")
-        gemm(Q, dS, dK, C, M, N, n, (C * N, N, 1), (N * M, M, 1), (C * M, M, 1), role="attn dk")
         grads = [None] * 5
         for i, (dX, Xh, P_) in ((2, (dQ, chat, N)), (3, (dK, shat, M)), (4, (dV, s, M))):
             if ctx.needs_input_grad[i]:

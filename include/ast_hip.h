@@ -394,6 +394,19 @@ int ast_instance_norm_backward_f32(const float* x, const float* mean, const floa
                                    float* dx, long long planes, long long hw, int accumulate, void* stream);
 /* dst += a * b elementwise. */
 int ast_fma_inplace_f32(float* dst, const float* a, const float* b, long long n, void* stream);
+/* Flash-style AdaAttN backward (csrc/adaattn_flash.hip; replaces the materialised P / dS of the
+ * calls above for large maps). q [n][C][N], k [n][C][M], vv [n][2C][M] ([V; V^2]) as above;
+ * C a multiple of 16, at most 128, not 80 or 112 (ast_adaattn_flash_supported).
+ * stats: o2 [n][N][2C] = softmax(Q^T K) [V; V^2]^T and lse2 [n][N] (log2-domain row log-sum-exp).
+ * bwd_kv: dk [n][C][M] = Q dS, dvv [n][2C][M] = dO^T P, from do2 / drow of ast_adaattn_dstats_f32.
+ * bwd_q: dq [n][C][N] = K dS^T. Deterministic (one lane sums each output in a fixed order). */
+int ast_adaattn_flash_supported(int c);
+int ast_adaattn_flash_stats_f32(const float* q, const float* k, const float* vv, float* o2, float* lse2, int n, int c,
+                                int nq, int nk, void* stream);
+int ast_adaattn_flash_bwd_kv_f32(const float* q, const float* k, const float* vv, const float* do2, const float* lse2,
+                                 const float* drow, float* dk, float* dvv, int n, int c, int nq, int nk, void* stream);
+int ast_adaattn_flash_bwd_q_f32(const float* q, const float* k, const float* vv, const float* do2, const float* lse2,
+                                const float* drow, float* dq, int n, int c, int nq, int nk, void* stream);
 
 size_t ast_adaattn_workspace_bytes(int dtype, int n, int c, int hc, int wc, int hs, int ws);
 int ast_adaattn_fwd(int dtype, const void* content, const void* style, const float* wq,
