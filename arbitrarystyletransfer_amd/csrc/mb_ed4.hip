@@ -573,6 +573,21 @@ int launch_s2(EdArgs a, hipStream_t st) {
 //    then + b2 (+ residual) as pw_kernel does: the output is bit-identical to expand_dw4 + se_fold +
 //    pw. 28 of the 32 columns are stored.
 // HBM traffic per block: x twice (both passes) and out once, against x, D written, D read and out.
+// Timing-only builds (scripts/build_variants.sh; wrong results): EDPW_T_NOSTORE drops the GEMM wave's
+// residual loads and output stores, EDPW_T_NOGEMM its MFMAs too, EDPW_T_NODW the compute waves'
+// depthwise FMAs.
+#ifndef EDPW_T_NOSTORE
+#define EDPW_T_NOSTORE 0
+#endif
+#ifndef EDPW_T_NOGEMM
+#define EDPW_T_NOGEMM 0
+#endif
+#ifndef EDPW_T_NODW
+#define EDPW_T_NODW 0
+#endif
+#ifndef EDPW_T_GEMM1
+#define EDPW_T_GEMM1 0  // the GEMM wave sums one 32-channel block instead of NCB
+#endif
 template <int KS, int NCB, int NCO>
 __global__ __launch_bounds__(64 * (NCB + 1)) __attribute__((amdgpu_waves_per_eu(3))) void expand_dw_pw4_kernel(
     EdpwArgs pa, int strips, int bands, int total) {
@@ -587,6 +602,7 @@ __global__ __launch_bounds__(64 * (NCB + 1)) __attribute__((amdgpu_waves_per_eu(
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   __shared__ __align__(16) bf16 dimg[2][NCB * 32 * DP];
   __shared__ __align__(16) bf16 wsm[NCO * 16 * WP];
+  __shared__ __align__(16) float ostg[NCO * 16 * 32];  // GEMM wave: a row's outputs [co][28 px] (+ b2)
   const EdArgs& a = pa.e;
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, cb = threadIdx.x >> 6;
   const int per = (total + 7) >> 3;
@@ -624,6 +640,73 @@ __global__ __launch_bounds__(64 * (NCB + 1)) __attribute__((amdgpu_waves_per_eu(
         const int co = 16 * m + 4 * g + j;
         bco[m][j] = (pa.b2 && co < pa.cout) ? pa.b2[co] : 0.f;
       }
+    // wo % 4 == 0 (every config-5 map): the row's outputs leave through ostg as 8-byte pieces of 4
+    // pixels (7 per channel row; the strip starts at a multiple of 28 columns) and the residual
+    // arrives the same way -- 2-byte scattered accesses made the stores the pass's largest cost
+    // (a timing build without them: 28.7 -> 20.1 ms per config-5 step). Same arithmetic and
+    // rounding as below: bit-identical.
+    if ((a.wo & 3) == 0) {
+      constexpr int NP = NCO * 16 * 7, PPL = (NP + 63) / 64;  // pieces per row, per lane
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      for (int orow = 0; orow < TH; ++orow) {
+        const int oy = y0 + orow;
+        const bool rowv = oy < a.ho;
+        unsigned poff[PPL];
+        u32x2 prv[PPL];
+#pragma unroll
+        for (int i = 0; i < PPL; ++i) {
+          const int p = lane + 64 * i, co = p / 7, seg = p - 7 * co, ox = x0 + 2 + 4 * seg;
+          poff[i] = (rowv && p < NP && co < pa.cout && ox < a.wo)
+                        ? (unsigned)(2 * (co * plane_o + (int64_t)oy * a.wo + ox)) : kDrop;
+          prv[i] = (pa.res && !EDPW_T_NOSTORE) ? __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)poff[i], 0, 0))
+                                               : u32x2{0u, 0u};
+        }
+        lds_barrier();  // row orow's image is complete
+        const bf16* img = dimg[orow & 1];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int col = (t & 1) * 16 + 4 * p4;
+          const bf16* wr = wsm + (t / 2 * 16 + (lane & 15)) * WP + 4 * g;
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kc = 0; kc < (EDPW_T_NOGEMM ? 0 : EDPW_T_GEMM1 ? 1 : NCB); ++kc) {
+            const s16x4 alo = *reinterpret_cast<const s16x4*>(wr + 32 * kc);
+            const s16x4 ahi = *reinterpret_cast<const s16x4*>(wr + 32 * kc + 16);
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (32 * kc + 4 * g + q4) * DP + col));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (32 * kc + 16 + 4 * g + q4) * DP + col));
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7)),
+                __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7)), acc, 0, 0, 0);
+          }
+          const int px = (t & 1) * 16 + (lane & 15);
+          if (px >= 2 && px < 2 + OW) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ostg[(t / 2 * 16 + 4 * g + j) * 32 + px - 2] = acc[j] + bco[t / 2][j];
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes are done
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < PPL; ++i) {
+          const int p = min(lane + 64 * i, NP - 1), co = p / 7, seg = p - 7 * co;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(ostg + co * 32 + 4 * seg);
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o[e] = v[e];
+            if (pa.res) {
+              const unsigned w = prv[i][e >> 1];
+              o[e] = o[e] + (float)__builtin_bit_cast(bf16, (unsigned short)(e & 1 ? w >> 16 : w & 0xffffu));
+            }
+          }
+          const u32x2 pk = {(unsigned)bf16_bits(o[0]) | ((unsigned)bf16_bits(o[1]) << 16),
+                            (unsigned)bf16_bits(o[2]) | ((unsigned)bf16_bits(o[3]) << 16)};
+          if (!EDPW_T_NOSTORE || o[0] == 1.2345e-30f)
+            __builtin_amdgcn_raw_buffer_store_b64(pk, orr, (int)poff[i], 0, 0);
+        }
+      }
+      return;
+    }
     for (int orow = 0; orow < TH; ++orow) {
       const int oy = y0 + orow;
       const bool rowv = oy < a.ho;
@@ -637,7 +720,8 @@ __global__ __launch_bounds__(64 * (NCB + 1)) __attribute__((amdgpu_waves_per_eu(
         for (int j = 0; j < 4; ++j) {
           const int co = t / 2 * 16 + 4 * g + j;
           off[t][j] = (ok && co < pa.cout) ? (unsigned)(2 * (co * plane_o + (int64_t)oy * a.wo + ox)) : kDrop;
-          rv[t][j] = pa.res ? __builtin_amdgcn_raw_buffer_load_b16(rr, (int)off[t][j], 0, 0) : (unsigned short)0;
+          rv[t][j] = (pa.res && !EDPW_T_NOSTORE) ? __builtin_amdgcn_raw_buffer_load_b16(rr, (int)off[t][j], 0, 0)
+                                                 : (unsigned short)0;
         }
       }
       lds_barrier();  // row orow's image is complete
@@ -648,7 +732,7 @@ __global__ __launch_bounds__(64 * (NCB + 1)) __attribute__((amdgpu_waves_per_eu(
         const bf16* wr = wsm + (t / 2 * 16 + (lane & 15)) * WP + 4 * g;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kc = 0; kc < NCB; ++kc) {
+        for (int kc = 0; kc < (EDPW_T_NOGEMM ? 0 : NCB); ++kc) {
           const s16x4 alo = *reinterpret_cast<const s16x4*>(wr + 32 * kc);
           const s16x4 ahi = *reinterpret_cast<const s16x4*>(wr + 32 * kc + 16);
           const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (32 * kc + 4 * g + q4) * DP + col));
@@ -661,7 +745,8 @@ __global__ __launch_bounds__(64 * (NCB + 1)) __attribute__((amdgpu_waves_per_eu(
         for (int j = 0; j < 4; ++j) {
           float o = acc[j] + bco[t / 2][j];
           if (pa.res) o = o + (float)__builtin_bit_cast(bf16, rv[t][j]);
-          __builtin_amdgcn_raw_buffer_store_b16(bf16_bits(o), orr, (int)off[t][j], 0, 0);
+          if (!EDPW_T_NOSTORE || o == 1.2345e-30f)
+            __builtin_amdgcn_raw_buffer_store_b16(bf16_bits(o), orr, (int)off[t][j], 0, 0);
         }
       }
     }
@@ -747,7 +832,8 @@ __global__ __launch_bounds__(64 * (NCB + 1)) __attribute__((amdgpu_waves_per_eu(
           for (int i = 0; i < 16; ++i) {
             float v = ky == 0 ? bd : acc[slot][i];
 #pragma unroll
-            for (int kx = 0; kx < K; ++kx) v = fmaf(wk[ky * K + kx], e[i + 2 - P + kx], v);
+            for (int kx = 0; kx < (EDPW_T_NODW ? (ky == 0 && kx == 0 ? 1 : 0) : K); ++kx)
+              v = fmaf(wk[ky * K + kx], e[i + 2 - P + kx], v);
             acc[slot][i] = v;
           }
         }

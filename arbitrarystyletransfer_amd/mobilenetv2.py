@@ -33,10 +33,10 @@ DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1}
 # once, write its output once) — bench.py's config-5 roofline denominator.
 IO_TRACE = None
 DW_TRACE = None   # bench.py: per expand_dw launch, the depthwise multiply-adds (VALU work)
-# AST_MB_EDPW=1: the fused block pair (ast_mb_expand_dw_pw: no hidden-width tensor in memory) for
-# the shapes it supports. Off by default: bit-identical, but measured 3% slower on the config-5 step
-# than expand_dw + se_fold + pw ("Fused block pair").
-FUSED_PAIR = os.environ.get("AST_MB_EDPW", "0") == "1"
+# The fused block pair (ast_mb_expand_dw_pw: no hidden-width tensor in memory) for the shapes it
+# supports, bit-identical to expand_dw + se_fold + pw; on by default since round 4 (its outputs leave
+# as 8-byte pieces: DESIGN.md §3, "Fused block pair"). AST_MB_EDPW=0 selects the unfused chain.
+FUSED_PAIR = os.environ.get("AST_MB_EDPW", "1") == "1"
 
 
 def _trace_io(nbytes: int) -> None:

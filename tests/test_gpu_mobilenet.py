@@ -96,6 +96,7 @@ FUSED_CASES = [
     (24, 24, 6, False, (2, 33, 57)),
     (24, 16, 6, True, (1, 64, 64)),      # no residual (cout != cin)
     (24, 24, 6, False, (1, 5, 7)),       # smaller than one strip and one band
+    (24, 24, 6, False, (1, 40, 60)),     # W % 4 == 0 (8-byte output pieces), residual, 4-column last strip
 ]
 
 
