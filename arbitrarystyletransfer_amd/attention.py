@@ -21,6 +21,7 @@ import torch
 
 from . import ops
 from ._lib import HipOpError, check, lib, ptr, stream_ptr
+from .functional import _grad_buffer
 from .mbtrain import gemm
 
 
@@ -57,6 +58,7 @@ class AdaAttNFn(torch.autograd.Function):
     def forward(ctx, c, s, wq, wk, wv):
         out = ops.adaattn(c, s, wq, wk, wv)
         ctx.save_for_backward(c, s, wq, wk, wv)
+        ctx.params = (wq, wk, wv)
         return out
 
     @staticmethod
@@ -116,10 +118,11 @@ class AdaAttNFn(torch.autograd.Function):
         grads = [None] * 5
         for i, (dX, Xh, P_) in ((2, (dQ, chat, N)), (3, (dK, shat, M)), (4, (dV, s, M))):
             if ctx.needs_input_grad[i]:
-                dW = torch.zeros((C, C), device=dev, dtype=torch.float32)
-                gemm(dX, Xh, dW, C, C, P_, n, (C * P_, P_, 1), (C * P_, 1, P_), (0, C, 1),
-                     ksplit=_wsplit(n, P_), accumulate=True, role="attn dw")
-                grads[i] = dW.view_as((wq, wk, wv)[i - 2]).to((wq, wk, wv)[i - 2].dtype)
+                wp = ctx.params[i - 2]
+                dW = _grad_buffer(wp, tuple(wp.shape), dX) if wp.dtype == torch.float32 else f(C, C)
+                gemm(dX, Xh, dW.view(C, C), C, C, P_, n, (C * P_, P_, 1), (C * P_, 1, P_), (0, C, 1),
+                     ksplit=_wsplit(n, P_), role="attn dw")
+                grads[i] = dW.view_as(wp).to(wp.dtype)
         if need_dc:
             dchat = f(n, C, N)
             gemm(Wq, dQ, dchat, C, N, C, n, (0, 1, C), (C * N, N, 1), (C * N, N, 1), role="attn dchat")

@@ -17,6 +17,7 @@ import torch.nn as nn
 
 from . import dp, ops
 from ._lib import HipOpError, check, lib, ptr, stream_ptr, workspace
+from .functional import _grad_buffer   # weight gradients straight into the DP / graph arena slice
 
 
 def _s(t):
@@ -70,6 +71,7 @@ class PwConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, x2 if x2 is not None else x, wt)
         ctx.has_x2 = x2 is not None
         ctx.wshape = weight.shape
+        ctx.param = weight
         return y
 
     @staticmethod
@@ -95,7 +97,7 @@ class PwConvFn(torch.autograd.Function):
         if ctx.has_x2:
             dx2 = grads[1]
         if ctx.needs_input_grad[2]:
-            dw = torch.empty((cout, cin), device=g.device, dtype=torch.float32)
+            dw = _grad_buffer(ctx.param, ctx.wshape, g).view(cout, cin)
             for xi, off in parts:
                 ci = xi.shape[1]
                 gemm(g, xi, dw[:, off:], cout, ci, n * P, 1, (cout * P, P, 1), (ci * P, 1, P), (0, cin, 1),
@@ -121,6 +123,7 @@ class DwConvFn(torch.autograd.Function):
               "dw conv")
         ctx.save_for_backward(x, wt)
         ctx.k, ctx.s, ctx.act, ctx.wshape = k, s, int(act), weight.shape
+        ctx.param = weight
         return y
 
     @staticmethod
@@ -134,7 +137,7 @@ class DwConvFn(torch.autograd.Function):
             check(lib().ast_mbt_dw_act_f32(1, ptr(x) if ctx.act else None, ptr(wt), ptr(g), ptr(dx), n, c, h, w, ctx.k,
                                            ctx.s, ctx.act, None, 0, _s(g)), "dw dgrad")
         if ctx.needs_input_grad[1]:
-            dw = torch.empty((c, ctx.k * ctx.k), device=g.device, dtype=torch.float32)
+            dw = _grad_buffer(ctx.param, ctx.wshape, g).view(c, ctx.k * ctx.k)
             ws = workspace(lib().ast_mbt_dw_workspace_floats(n, c, h, w, ctx.k), x.device)
             check(lib().ast_mbt_dw_act_f32(2, ptr(x), ptr(wt), ptr(g), ptr(dw), n, c, h, w, ctx.k, ctx.s, ctx.act,
                                            ptr(ws), ws.numel(), _s(g)), "dw wgrad")
@@ -186,6 +189,7 @@ class BatchNormTrainFn(torch.autograd.Function):
         if track:
             bn.num_batches_tracked.add_(1)   # bookkeeping counter (torch does the same host-side increment)
         ctx.save_for_backward(x, gamma, beta, mean, invstd, inv_count if inv_count is not None else mean)
+        ctx.params = (gamma, beta)
         return y
 
     @staticmethod
@@ -196,8 +200,8 @@ class BatchNormTrainFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         ws = _bn_workspace(x, n, c, h * w)
         if ctx.group is None:
-            dgamma = torch.empty_like(mean)
-            dbeta = torch.empty_like(mean)
+            dgamma = _grad_buffer(ctx.params[0], (c,), mean)
+            dbeta = _grad_buffer(ctx.params[1], (c,), mean)
             check(lib().ast_mbt_bn_act_bwd_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma),
                                                ptr(beta), ctx.act, ptr(dgamma), ptr(dbeta), ptr(dx), ptr(ws),
                                                ws.numel(), _s(g)), "batch norm backward")
@@ -207,7 +211,10 @@ class BatchNormTrainFn(torch.autograd.Function):
         check(L.ast_mbt_bn_act_bwd_sums_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma),
                                             ptr(beta), ctx.act, ptr(ws), ws.numel(), ptr(sums), _s(g)),
               "bn backward sums")
-        dbeta, dgamma = sums[0].clone(), sums[1].clone()     # local: the gradient all-reduce averages them
+        dgamma = _grad_buffer(ctx.params[0], (c,), mean)
+        dbeta = _grad_buffer(ctx.params[1], (c,), mean)
+        dbeta.copy_(sums[0])      # local: the gradient all-reduce averages them
+        dgamma.copy_(sums[1])
         dp.all_reduce_sum(sums, ctx.group)
         check(L.ast_mbt_bn_act_bwd_apply_f32(ptr(x), ptr(g), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma),
                                              ptr(beta), ctx.act, ptr(sums), ptr(inv_count), ptr(dx), _s(g)),
@@ -294,6 +301,7 @@ class SEFn(torch.autograd.Function):
                                       _s(x)), "se scale")
         ctx.save_for_backward(x, w1c, w2c, pool, hid, z, gate)
         ctx.act = act
+        ctx.params = (w1, b1, w2, b2)
         return y
 
     @staticmethod
@@ -306,8 +314,9 @@ class SEFn(torch.autograd.Function):
         dgate = torch.empty((n, c), device=x.device, dtype=torch.float32)
         check(L.ast_mbt_plane_act_f32(4 if ctx.act else 1, ptr(g), ptr(x), None, None, None, ptr(dgate), n * c, h * w,
                                       _s(g)), "se dgate")
-        dw1, db1 = torch.empty_like(w1), torch.empty((red,), device=x.device, dtype=torch.float32)
-        dw2, db2 = torch.empty_like(w2), torch.empty((c,), device=x.device, dtype=torch.float32)
+        pw1, pb1, pw2, pb2 = ctx.params
+        dw1, db1 = _grad_buffer(pw1, tuple(w1.shape), x), _grad_buffer(pb1, (red,), x)
+        dw2, db2 = _grad_buffer(pw2, tuple(w2.shape), x), _grad_buffer(pb2, (c,), x)
         dpool = torch.empty((n, c), device=x.device, dtype=torch.float32)
         ws = workspace(n * (c + red), x.device)
         check(L.ast_mbt_se_fc_bwd_f32(ptr(dgate), ptr(z), ptr(hid), ptr(pool), ptr(w1), ptr(w2), n, c, red, h * w,
