@@ -45,6 +45,7 @@ m = synth.live_init_(models.AdaAttN(C), 7).to(dev)
 with torch.no_grad():
     m.W_q.weight.mul_(0.125)
     m.W_k.weight.mul_(0.125)
+torch.manual_seed(0)
 c = torch.rand(n, C, H, H, device=dev).requires_grad_()
 s = torch.rand(n, C, H, H, device=dev).requires_grad_()
 g = torch.rand(n, C, H, H, device=dev) - 0.5
