@@ -176,9 +176,35 @@ def workspace(nfloats: int, device) -> "torch.Tensor":
 _ACC_FLOATS = None
 
 
+_ACC_POOL = None   # [chunk, next row] while an accumulator_pool() scope is active
+
+
 def loss_accumulator(device) -> "torch.Tensor":
-    """A zeroed loss accumulator (AST_LOSS_ACC_FLOATS floats; the value is element 0)."""
+    """A zeroed loss accumulator (AST_LOSS_ACC_FLOATS floats; the value is element 0). Inside an
+    accumulator_pool() scope it is a row of a chunk of 64 zeroed at once."""
     global _ACC_FLOATS
     if _ACC_FLOATS is None:
         _ACC_FLOATS = int(lib().ast_loss_acc_floats())
+    pool = _ACC_POOL
+    if pool is not None:
+        chunk, i = pool.get(device, (None, 64))
+        if i == 64:
+            chunk, i = torch.zeros((64, _ACC_FLOATS), device=device, dtype=torch.float32), 0
+        pool[device] = (chunk, i + 1)
+        return chunk[i]
     return torch.zeros((_ACC_FLOATS,), device=device, dtype=torch.float32)
+
+
+class accumulator_pool:
+    """Scope of one training step: its loss accumulators come from chunks of 64 zeroed by one
+    launch each (~40 loss terms per ASTTrainer step, each a zero fill before). Every scope takes
+    fresh chunks, so values a caller keeps from an earlier step are never overwritten."""
+
+    def __enter__(self):
+        global _ACC_POOL
+        self.prev, _ACC_POOL = _ACC_POOL, {}
+        return self
+
+    def __exit__(self, *exc):
+        global _ACC_POOL
+        _ACC_POOL = self.prev

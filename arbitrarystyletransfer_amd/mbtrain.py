@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from . import dp, ops
-from ._lib import HipOpError, check, lib, ptr, stream_ptr, workspace
+from ._lib import HipOpError, accumulator_pool, check, lib, ptr, stream_ptr, workspace
 from .functional import _grad_buffer   # weight gradients straight into the DP / graph arena slice
 
 
@@ -145,6 +145,40 @@ class DwConvFn(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+# BatchNorm's num_batches_tracked bookkeeping (torch increments it on every train-mode forward): a
+# trainer step defers the increments and applies them as one multi-tensor add at its end (one launch
+# instead of one per BatchNorm call: 84 per ASTTrainer step); outside a step each call adds at once.
+_BN_PENDING = None
+
+
+def _bump_batches_tracked(bn):
+    if _BN_PENDING is None:
+        bn.num_batches_tracked.add_(1)
+    else:
+        t = bn.num_batches_tracked
+        _BN_PENDING[id(t)] = (t, _BN_PENDING.get(id(t), (t, 0))[1] + 1)
+
+
+class deferred_bn_counters:
+    """Context of one training step: the num_batches_tracked increments of every train-mode
+    BatchNorm call inside it become one torch._foreach_add_ on exit (a BatchNorm run twice in the
+    step -- the AST encoder over the content and over the stylised image -- counts twice)."""
+
+    def __enter__(self):
+        global _BN_PENDING
+        self.prev, _BN_PENDING = _BN_PENDING, {}
+        self.pool = accumulator_pool().__enter__()   # and the step's loss accumulators, pooled
+        return self
+
+    def __exit__(self, *exc):
+        global _BN_PENDING
+        self.pool.__exit__(*exc)
+        pend, _BN_PENDING = _BN_PENDING, self.prev
+        if pend:
+            ts = [t for t, _ in pend.values()]
+            torch._foreach_add_(ts, [k for _, k in pend.values()])
+
+
 def _bn_workspace(x, n, c, hw):
     return torch.empty((max(1, lib().ast_mbt_bn_workspace_floats(n, c, hw)),), device=x.device, dtype=torch.float32)
 
@@ -187,7 +221,7 @@ class BatchNormTrainFn(torch.autograd.Function):
             check(L.ast_mbt_bn_act_apply_f32(ptr(x), n, c, h * w, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
                                              ctx.act, ptr(y), _s(x)), "bn apply")
         if track:
-            bn.num_batches_tracked.add_(1)   # bookkeeping counter (torch does the same host-side increment)
+            _bump_batches_tracked(bn)   # bookkeeping counter (torch does the same increment)
         ctx.save_for_backward(x, gamma, beta, mean, invstd, inv_count if inv_count is not None else mean)
         ctx.params = (gamma, beta)
         return y

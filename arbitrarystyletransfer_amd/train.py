@@ -37,9 +37,9 @@ import os
 import torch
 import torch.distributed as dist
 
-from . import dp
+from . import _lib, dp
 from . import losses as L
-from . import models, ops
+from . import mbtrain, models, ops
 from .conf import enc_out_layers
 from .optim import FusedAdam
 
@@ -216,7 +216,8 @@ class AdaINTrainer:
         return (b - a) / self.args.batch_size
 
     def train_step(self, content, style, record=False):
-        out = self.compute_losses(content, style)
+        with _lib.accumulator_pool():
+            out = self.compute_losses(content, style)
         self.optim.zero_grad(set_to_none=True)
         w = self.shard_weight(content.shape[0])
         if w == 1.0:
@@ -396,7 +397,8 @@ class ASTTrainer:
 
     def _step_body(self, content, style):
         """The captured step (StepGraph): losses, backward, reduction, clip + Adam."""
-        out = self.compute_losses(content, style)
+        with mbtrain.deferred_bn_counters():
+            out = self.compute_losses(content, style)
         self._backward(out, content.shape[0])
         self.ast_optim.step_static()
         return out
@@ -405,7 +407,8 @@ class ASTTrainer:
         if self.graph:
             out = self._step_graph.run(content, style)
         else:
-            out = self.compute_losses(content, style)
+            with mbtrain.deferred_bn_counters():
+                out = self.compute_losses(content, style)
             self.ast_optim.zero_grad(set_to_none=True)                                  # :287
             self._backward(out, content.shape[0])
             if self.grad_hook is not None:
@@ -501,7 +504,8 @@ class AutoencoderTrainer:
         return {"loss": loss, "recon_loss": recon_loss, "content_loss": content_loss, "recon": recon_imgs}
 
     def train_step(self, content_imgs, record=True):
-        out = self.compute_losses(content_imgs)
+        with mbtrain.deferred_bn_counters():
+            out = self.compute_losses(content_imgs)
         self.ae_optim.zero_grad(set_to_none=True)
         if self.world == 1:
             out["loss"].backward()

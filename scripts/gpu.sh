@@ -9,6 +9,7 @@
 #   bench            bench.py default line (config 2, with its CPU baseline, as the driver runs it)
 #   bench:MODE       bench.py --mode MODE (no CPU baseline): train, mobilenet, ast-train, ae-train
 #   profiles         rocprofv3 kernel-trace stats + FETCH/WRITE_SIZE passes (scripts/measure_profiles.sh)
+#   clock            effective clock and MFMA busy of the config-2 conv dispatches (scripts/pmc_clock.sh)
 #   race             scripts/debug/race_probe4.py (16 repeats) and dp_repeat.py (8 runs) beside a
 #                    background config-3 bench (the concurrent-load condition of DESIGN.md §4)
 #   race:idle        the same probes with no background load
@@ -63,6 +64,7 @@ for task in "$@"; do
       timeout -k 10 300 python bench.py --mode $m --cpu-seconds 0 > $OUT/${TAG}_bench_$m.json 2> $OUT/${TAG}_bench_$m.err || exit 1
       cut -c1-400 $OUT/${TAG}_bench_$m.json ;;
     profiles) bash scripts/measure_profiles.sh ${TAG}m || exit 1 ;;
+    clock) bash scripts/pmc_clock.sh ${TAG} fwd conv3x3 > $OUT/${TAG}_clock.txt 2>&1; rc=$?; cat $OUT/${TAG}_clock.txt; [ $rc -eq 0 ] || exit 1 ;;
     race) run_race load "" || exit 1 ;;
     race:idle) run_race idle _idle || exit 1 ;;
     race:split)  # the probes on CUs 0-127, the load on CUs 128-255 (HSA_CU_MASK): no CU shared
