@@ -648,6 +648,10 @@ __global__ __launch_bounds__(64 * (NCB + 1)) __attribute__((amdgpu_waves_per_eu(
     if ((a.wo & 3) == 0) {
       constexpr int NP = NCO * 16 * 7, PPL = (NP + 63) / 64;  // pieces per row, per lane
       typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      // the A fragments (wg[n], the same for every row) stay in registers: read once, after the first
+      // row barrier (which also orders wsm's staging), instead of per row. (Every wave of the
+      // workgroup must pass the same number of barriers: no extra one here.)
+      s16x4 afr[NCO][NCB][2];
       for (int orow = 0; orow < TH; ++orow) {
         const int oy = y0 + orow;
         const bool rowv = oy < a.ho;
@@ -662,16 +666,26 @@ __global__ __launch_bounds__(64 * (NCB + 1)) __attribute__((amdgpu_waves_per_eu(
                                                : u32x2{0u, 0u};
         }
         lds_barrier();  // row orow's image is complete
+        if (orow == 0) {
+#pragma unroll
+          for (int m = 0; m < NCO; ++m) {
+            const bf16* wr = wsm + (m * 16 + (lane & 15)) * WP + 4 * g;
+#pragma unroll
+            for (int kc = 0; kc < NCB; ++kc) {
+              afr[m][kc][0] = *reinterpret_cast<const s16x4*>(wr + 32 * kc);
+              afr[m][kc][1] = *reinterpret_cast<const s16x4*>(wr + 32 * kc + 16);
+            }
+          }
+        }
         const bf16* img = dimg[orow & 1];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const int col = (t & 1) * 16 + 4 * p4;
-          const bf16* wr = wsm + (t / 2 * 16 + (lane & 15)) * WP + 4 * g;
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int kc = 0; kc < (EDPW_T_NOGEMM ? 0 : EDPW_T_GEMM1 ? 1 : NCB); ++kc) {
-            const s16x4 alo = *reinterpret_cast<const s16x4*>(wr + 32 * kc);
-            const s16x4 ahi = *reinterpret_cast<const s16x4*>(wr + 32 * kc + 16);
+            const s16x4 alo = afr[t / 2][kc][0];
+            const s16x4 ahi = afr[t / 2][kc][1];
             const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (32 * kc + 4 * g + q4) * DP + col));
             const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (32 * kc + 16 + 4 * g + q4) * DP + col));
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
