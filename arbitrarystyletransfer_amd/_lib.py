@@ -179,13 +179,14 @@ _ACC_FLOATS = None
 _ACC_POOL = None   # [chunk, next row] while an accumulator_pool() scope is active
 
 
-def loss_accumulator(device) -> "torch.Tensor":
+def loss_accumulator(device, pooled: bool = True) -> "torch.Tensor":
     """A zeroed loss accumulator (AST_LOSS_ACC_FLOATS floats; the value is element 0). Inside an
-    accumulator_pool() scope it is a row of a chunk of 64 zeroed at once."""
+    accumulator_pool() scope it is a row of a chunk of 64 zeroed at once -- not for the outputs of
+    torch.ops custom operators (pooled=False), which must not share storage with each other."""
     global _ACC_FLOATS
     if _ACC_FLOATS is None:
         _ACC_FLOATS = int(lib().ast_loss_acc_floats())
-    pool = _ACC_POOL
+    pool = _ACC_POOL if pooled else None
     if pool is not None:
         chunk, i = pool.get(device, (None, 64))
         if i == 64:

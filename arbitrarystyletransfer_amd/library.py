@@ -196,7 +196,7 @@ register_autograd("ast_hip::gram", _gram_backward, setup_context=_gram_setup)
 # ------------------------------------------------------------------------------------------------
 
 def _acc(like):
-    return loss_accumulator(like.device)
+    return loss_accumulator(like.device, pooled=False)   # custom-op outputs: storage of their own
 
 
 @custom_op("ast_hip::content_mvn_loss", mutates_args=())
