@@ -31,6 +31,7 @@ for uneven shards too.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 
@@ -65,6 +66,11 @@ class StepGraph:
         return ([tuple(x.shape) for x in inputs], self.optim.static_hyper())
 
     def _capture(self, inputs):
+        # a recapture (new input shapes or optimizer hyper-parameters) first drops the old graph,
+        # its static buffers and outputs (the caller holds copies), so nothing of the old graph's
+        # memory pool is released while the new capture is underway
+        self.graph = self.out = self.static = None
+        gc.collect()
         for net in self.frozen:
             net.prepack()
         self.optim.zero_grad(set_to_none=True)
@@ -77,8 +83,12 @@ class StepGraph:
             s_.copy_(x)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.out = self.body(*self.static)
+        gc.disable()   # no finalizer of unrelated garbage may run (and free or sync) inside the capture
+        try:
+            with torch.cuda.graph(g):
+                self.out = self.body(*self.static)
+        finally:
+            gc.enable()
         self.optim.fill_static()
         self.graph = g
         self.key = self._key(inputs)
