@@ -886,6 +886,270 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   }
 }
 
+// Persistent form of the M16 split-bf16 kernel (round 4). One workgroup per CU
+// slot walks the blocks b = blockIdx.x + k * gridDim.x (same XCD for all of them: b % 8 is fixed,
+// and decode_block keeps the output-channel groups of a pixel tile on one XCD), and per block:
+//   * the NEXT block's first K-chunk (its gather and weight slab) is loaded during the current
+//     block's last chunk of MFMAs, so no block starts with an unoverlapped gather;
+//   * the epilogue's global stores are left in flight (LDS-only barriers after it), so the store
+//     tail of one block runs under the next block's first MFMAs instead of holding the CU.
+// Per block the arithmetic, k order and rounding are conv3x3_x3_kernel<M16>'s: bit-identical.
+// Measured on config 2 (profiles/r04_conv_persistent.txt): 1-2 % SLOWER per dispatch than the
+// one-block-per-workgroup form, also on grids of one block per slot, so the loss is per-block code
+// (argument re-reads, per-block address recomputation), not the static block walk; opt-in only
+// (AST_CONV_PERSIST=1 maps 28-31 to 32-35).
+__device__ __forceinline__ void x3_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// The kernel's ConvArgs re-read from the kernarg segment at the point of use: the empty asm hides the
+// pointer's provenance, so the compiler cannot hoist the argument loads out of the block loop and keep
+// every field in SGPRs across it (the persistent loop otherwise runs out of SGPRs and spills).
+// A wave-uniform pointer the divergence analysis cannot see as one (it is assigned under the block
+// loop's control flow): pinned to SGPRs, so the buffer descriptors built from it need no
+// readfirstlane loop per load.
+__device__ __forceinline__ const float* x3p_uniform(const float* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ const ConvArgs& x3p_args() {
+  auto p = __builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const ConvArgs*)p;
+}
+
+template <int WM, int RM, int RN, int UP, int OCC>
+__global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3p_kernel(ConvArgs, int nblk) {
+#define A_ x3p_args()
+  using C = X3Cfg<WM, RM, RN, UP>;
+  constexpr int NT = C::NT, TH = C::TH, BN = C::BN, SR = C::SR, SC = C::SC, A_PLANE = C::A_PLANE;
+  constexpr int A_T = C::A_T, B_T = C::B_T;
+  constexpr int Q = 2 * RN;
+  static_assert(RM % 2 == 0, "even rows per wave (pool windows, upsample row pairs)");
+  extern __shared__ __attribute__((aligned(16))) u32x4 x3_smem[];
+  u32x4* As = x3_smem;
+  u32x4* Bs = x3_smem + C::A_UNITS;
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+  const int tid = threadIdx.x, wm = tid >> 6, lane = tid & 63;
+  const int nch = (A_.Cin + kX3K - 1) / kX3K;
+
+  // the blocks of this workgroup: b = blockIdx.x + k * gridDim.x; a padding block (tile >= ntiles)
+  // is only ever followed by padding blocks, so the walk ends at the first one
+#define X3P_DECODE(B, OK, X0, Y0, IMG, N0)                                                            \
+  {                                                                                                 \
+    int t_, grp_;                                                                                   \
+    OK = (B) < nblk && decode_block((B), A_.tiles_x * A_.tiles_y * A_.N, (A_.Cout + BN - 1) / BN, t_, grp_);                                 \
+    if (OK) {                                                                                       \
+      X0 = (t_ % A_.tiles_x) * TW;                                                                   \
+      t_ /= A_.tiles_x;                                                                              \
+      Y0 = (t_ % A_.tiles_y) * TH;                                                                   \
+      IMG = t_ / A_.tiles_y;                                                                           \
+      N0 = grp_ * BN;                                                                               \
+    }                                                                                               \
+  }
+  // gather state of the block whose chunks are being loaded
+  unsigned g_off[A_T], g_pix[A_T];
+  int g_lds[A_T], g_h[A_T];
+  bool g_ok[A_T];
+  int b_src[B_T];
+  const float* __restrict__ xin = A_.x;
+#define X3P_SETUP(X0, Y0, IMG, N0)                                                                   \
+  {                                                                                                 \
+    const int plane_in = (A_.Hin * A_.Win), Hin = A_.Hin, Win = A_.Win;                                \
+    xin = x3p_uniform((IMG) < A_.nsplit ? A_.x + (int64_t)(IMG) * A_.Cin * plane_in                      \
+                                     : A_.x2 + (int64_t)((IMG) - A_.nsplit) * A_.Cin * plane_in);        \
+    const int sx0_ = (X0) / UP, sy0_ = (Y0) / UP - 1;                                               \
+    int tv_ = tid; /* laundered: the per-thread item decode is redone here, not hoisted and spilled */ \
+    asm volatile("" : "+v"(tv_));                                                                   \
+    _Pragma("unroll") for (int i = 0; i < A_T; ++i) {                                               \
+      const int e = min(tv_ + i * NT, A_PLANE - 1);                                                 \
+      const int c = e % SC, rest = e / SC, r = rest % SR, hh = rest / SR;                           \
+      const int sy = src_index<UP>(sy0_ + r, Hin, A_.reflect), sx = src_index<UP>(sx0_ - 1 + c, Win, A_.reflect); \
+      g_ok[i] = sy >= 0 && sx >= 0;                                                                 \
+      g_pix[i] = (unsigned)(max(sy, 0) * Win + max(sx, 0));                                         \
+      g_off[i] = g_ok[i] ? 4u * (unsigned)(8 * hh * plane_in) + 4u * g_pix[i] : 0x7ffffff0u;        \
+      g_lds[i] = e;                                                                                 \
+      g_h[i] = hh;                                                                                  \
+    }                                                                                               \
+    _Pragma("unroll") for (int i = 0; i < B_T; ++i) {                                               \
+      const int u = min(tv_ + i * NT, C::B_UNITS - 1), row = u / BN, j = u - row * BN;              \
+      b_src[i] = 16 * (row * A_.cout_pad + (N0) + j);                                                \
+    }                                                                                               \
+  }
+  float ra[A_T][8];
+  u32x4 rb[B_T];
+#define X3P_LOAD(KC)                                                                                    \
+  {                                                                                                     \
+    const int ci0 = (KC) * kX3K, plane_in = (A_.Hin * A_.Win), plane_b = 4 * plane_in;                       \
+    const int64_t chunk_units = ((int64_t)C::B_ROWS * A_.cout_pad);                                                        \
+    const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(                             \
+        const_cast<float*>(A_.wp + x3_split_offset(A_.Cin, A_.Cout)), 0,                               \
+        (int)min<int64_t>(0x7fffffff, (int64_t)nch * chunk_units * 16), 0x00020000);                   \
+    if (ci0 + kX3K <= A_.Cin) {                                                                          \
+      const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(                              \
+          const_cast<float*>(xin + (int64_t)ci0 * plane_in), 0, kX3K * plane_b, 0x00020000);           \
+      _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                     \
+        _Pragma("unroll") for (int i = 0; i < A_T; ++i)                                                 \
+          ra[i][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)g_off[i], j * plane_b, 0)); \
+    } else {                                                                                            \
+      _Pragma("unroll") for (int i = 0; i < A_T; ++i)                                                   \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                   \
+          ra[i][j] = xin[(int64_t)min(ci0 + 8 * g_h[i] + j, A_.Cin - 1) * plane_in + g_pix[i]];          \
+    }                                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < B_T; ++i)                                                     \
+      rb[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, b_src[i], (int)((KC) * chunk_units * 16), 0)); \
+  }
+#define X3P_STORE(KC)                                                                                   \
+  {                                                                                                     \
+    const ConvArgs& ka_ = x3p_args(); /* one laundered argument pointer per expansion */                \
+    _Pragma("unroll") for (int i = 0; i < A_T; ++i) {                                                   \
+      if (tid + i * NT < A_PLANE) {                                                                     \
+        if ((KC) * kX3K + kX3K > ka_.Cin) {                                                               \
+          const int cn = ka_.Cin - (KC) * kX3K - 8 * g_h[i];                                              \
+          _Pragma("unroll") for (int j = 0; j < 8; ++j) ra[i][j] = (g_ok[i] && j < cn) ? ra[i][j] : 0.f; \
+        }                                                                                               \
+        bf16x8 pv[3];                                                                                   \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                 \
+          bf16 t0, t1, t2;                                                                              \
+          split3(ra[i][j], t0, t1, t2);                                                                 \
+          pv[0][j] = t0;                                                                                \
+          pv[1][j] = t1;                                                                                \
+          pv[2][j] = t2;                                                                                \
+        }                                                                                               \
+        _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                   \
+          As[p * A_PLANE + g_lds[i]] = __builtin_bit_cast(u32x4, pv[p]);                                \
+      }                                                                                                 \
+    }                                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < B_T; ++i)                                                     \
+      if (tid + i * NT < C::B_UNITS) Bs[tid + i * NT] = rb[i];                                          \
+  }
+
+  int b = blockIdx.x, x0 = 0, y0 = 0, n = 0, n0 = 0;
+  bool ok;
+  X3P_DECODE(b, ok, x0, y0, n, n0);
+  if (!ok) return;  // uniform: the whole workgroup
+  X3P_SETUP(x0, y0, n, n0);
+  X3P_LOAD(0);
+  X3P_STORE(0);
+  x3_lds_barrier();
+  while (true) {
+    const int b2 = b + gridDim.x;
+    int nx0 = 0, ny0 = 0, nn = 0, nn0 = 0;
+    bool has_next;
+    X3P_DECODE(b2, has_next, nx0, ny0, nn, nn0);
+    // the MFMA loop's LDS addresses derive from lane values laundered per block, so they are
+    // recomputed here rather than hoisted out of the block loop and held live through the epilogue
+    int lv = lane, wv = wm;
+    asm volatile("" : "+v"(lv), "+v"(wv));
+    const int ml16 = lv & 15, mg16 = lv >> 4, mhh16 = mg16 & 1;
+    const int apl1 = (mg16 < 2 ? 0 : 1) * A_PLANE, apl2 = (mg16 < 2 ? 0 : 2) * A_PLANE;  // [hi|mid], [hi|lo]
+    const int bpl1 = 0, bpl2 = mg16 < 2 ? 1 : 0, bpl3 = mg16 < 2 ? 2 : 1;              // [hi;hi], [mid;hi], [lo;mid]
+    const int srow0 = wv * RM / UP;
+    int acol16[2][3];
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) acol16[pt][kx] = ((x0 + 16 * pt + ml16 + kx - 1) >> (UP - 1)) - x0 / UP + 1;
+    f32x4v acc16[RM][2][Q];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+        for (int q = 0; q < Q; ++q) acc16[i][pt][q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < nch; ++kc) {
+      if (kc + 1 < nch) X3P_LOAD(kc + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int tap = ky * 3 + kx;
+          bf16x8 g1[Q], g2[Q], g3[Q];
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            const int col = q * 16 + ml16;
+            g1[q] = __builtin_bit_cast(bf16x8, Bs[((bpl1 * 9 + tap) * 2 + mhh16) * BN + col]);
+            g2[q] = __builtin_bit_cast(bf16x8, Bs[((bpl2 * 9 + tap) * 2 + mhh16) * BN + col]);
+            g3[q] = __builtin_bit_cast(bf16x8, Bs[((bpl3 * 9 + tap) * 2 + mhh16) * BN + col]);
+          }
+#pragma unroll
+          for (int i = 0; i < RM; ++i) {
+            const int srow = (mhh16 * SR + srow0 + x3_srel<UP>(i, ky)) * SC;
+            bf16x8 f1[2], f2[2];
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) {
+              f1[pt] = __builtin_bit_cast(bf16x8, As[apl1 + srow + acol16[pt][kx]]);
+              f2[pt] = __builtin_bit_cast(bf16x8, As[apl2 + srow + acol16[pt][kx]]);
+            }
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+              for (int q = 0; q < Q; ++q) {
+                f32x4v c = acc16[i][pt][q];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g3[q], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[pt], g2[q], c, 0, 0, 0);
+                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g1[q], c, 0, 0, 0);
+              }
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (kc + 1 < nch) {  // LDS-only barriers: the previous block's epilogue stores keep draining
+        x3_lds_barrier();  // every wave is done reading this chunk
+        X3P_STORE(kc + 1);
+        x3_lds_barrier();
+      }
+    }
+    // epilogue: as conv3x3_x3_kernel<M16>, but every accumulator goes to the wave's LDS region first
+    // (RN x 32 channels: the accumulators are dead before the stores, while the next block's first
+    // chunk is held in registers), and the global stores are left in flight
+    if (has_next) {  // the next block's first chunk, in flight during this block's epilogue
+      X3P_SETUP(nx0, ny0, nn, nn0);
+      X3P_LOAD(0);
+    }
+    x3_lds_barrier();  // every wave is done reading the last chunk's tiles
+    int el = lane, ew = wm;  // laundered as in the MFMA loop
+    asm volatile("" : "+v"(el), "+v"(ew));
+    const int el16 = el & 15, eg16 = el >> 4;
+    float* region = reinterpret_cast<float*>(x3_smem) + ew * 32 * RM * 36;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        const int q = 2 * j + qq, co = n0 + 16 * q + el16;
+        const float bv = (co < A_.Cout && A_.bias) ? A_.bias[co] : 0.f;
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int pt = 0; pt < 2; ++pt) {
+            const f32x4v v = acc16[i][pt][q];
+            *reinterpret_cast<float4*>(region + ((16 * qq + el16) * RM + i) * 36 + 16 * pt + 4 * eg16) =
+                make_float4(v[0] + bv, v[1] + bv, v[2] + bv, v[3] + bv);
+          }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      store_region<RM>(A_, region, n, x0, y0, ew * RM, n0 + 32 * j, el);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!has_next) break;
+    x3_lds_barrier();  // every wave is done with its epilogue region (the stores stay in flight)
+    X3P_STORE(0);      // the next block's first chunk (loaded during the last MFMAs)
+    x3_lds_barrier();
+    b = b2;
+    x0 = nx0;
+    y0 = ny0;
+    n = nn;
+    n0 = nn0;
+  }
+#undef X3P_DECODE
+#undef X3P_SETUP
+#undef X3P_LOAD
+#undef X3P_STORE
+#undef A_
+}
+
 // Direct (VALU) 3x3 conv for cout <= 4 — the decoder's final 64->3 conv (models.py:627). As a
 // GEMM its N = 3 would leave >90% of every MFMA tile idle; as a direct conv each thread makes
 // 4 adjacent output pixels x COUT channels, weights are wave-uniform scalar loads, and the kernel
@@ -1290,6 +1554,44 @@ int launch_x3_one(const ConvArgs& a0, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// persistent form: one workgroup per CU slot (OCC per CU), a multiple of 8 (XCD-consistent stride)
+template <int WM, int RM, int RN, int UP, int OCC>
+int launch_x3p_one(const ConvArgs& a0, hipStream_t s) {
+  using C = X3Cfg<WM, RM, RN, UP>;
+  ConvArgs a = a0;
+  a.tiles_x = cdiv(a.W, TW);
+  a.tiles_y = cdiv(a.H, C::TH);
+  if (cdiv(a.Cout, C::BN) * C::BN > a.cout_pad) return AST_E_UNSUPPORTED;
+  const int64_t ntiles = (int64_t)a.tiles_x * a.tiles_y * a.N;
+  const int64_t nblk = (ntiles + 7) / 8 * 8 * cdiv(a.Cout, C::BN);
+  if (nblk >= 0x7fffffff) return AST_E_SHAPE;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  const int64_t slots = (int64_t)(cus + 7) / 8 * 8 * OCC;
+  const unsigned grid = (unsigned)(nblk < slots ? nblk : slots);
+  auto kern = conv3x3_x3p_kernel<WM, RM, RN, UP, OCC>;
+  constexpr int lds = C::LDS_BYTES;
+  static_assert(lds * OCC <= 160 * 1024, "LDS per CU");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(C::NT), lds, s, a, (int)nblk);
+  return (int)hipGetLastError();
+}
+
+template <int WM, int RM, int RN, int OCC = 1>
+int launch_x3p(const ConvArgs& a, hipStream_t s, int up) {
+  if (a.in_mean) return AST_E_UNSUPPORTED;
+  if ((int64_t)a.Cin * a.Hin * a.Win * 4 >= ((int64_t)1 << 31)) return AST_E_UNSUPPORTED;  // 32-bit buffer offsets
+  return up == 2 ? launch_x3p_one<WM, RM, RN, 2, OCC>(a, s) : launch_x3p_one<WM, RM, RN, 1, OCC>(a, s);
+}
+
 // split-bf16 MFMA kernel: no fused input normalisation (conv_1 runs the direct cin<=4 kernel)
 template <int WM, int RM, int RN, int OCC = 1, bool M16 = false>
 int launch_x3(const ConvArgs& a, hipStream_t s, int up) {
@@ -1343,6 +1645,11 @@ const CfgEntry kConfigs[] = {
     {launch_x3<4, 2, 2, 1, true>, 64, 8, 2, 0},         // 29: as 25
     {launch_x3<4, 2, 1, 2, true>, 32, 8, 2, 0},         // 30: as 26
     {launch_x3<8, 2, 1, 1, true>, 32, 16, 2, 0},        // 31: as 27
+    // persistent forms of 28-31 (next block's first chunk under the last MFMAs, store tail overlapped)
+    {launch_x3p<8, 2, 2>, 64, 16, 2, 0},                // 32: as 28
+    {launch_x3p<4, 2, 2>, 64, 8, 2, 0},                 // 33: as 29
+    {launch_x3p<4, 2, 1, 2>, 32, 8, 2, 0},              // 34: as 30
+    {launch_x3p<8, 2, 1, 1>, 32, 16, 2, 0},             // 35: as 31
 };
 constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -1426,6 +1733,11 @@ int ast_conv3x3_fwd_f32_cfg(int cfg, const float* x, const float* x2, int n2, co
   }();
   if (cfg >= 24 && cfg <= 27 && m16 == 1) cfg += 4;
   if (cfg >= 28 && cfg <= 31 && m16 == 0) cfg -= 4;
+  static const int persist = [] {  // AST_CONV_PERSIST=1: the M16 tiles 28-31 in their persistent form 32-35
+    const char* v = getenv("AST_CONV_PERSIST");
+    return v ? atoi(v) : 0;
+  }();
+  if (cfg >= 28 && cfg <= 31 && persist == 1) cfg += 4;
   const CfgEntry& e = kConfigs[cfg];
   if (y_pool && (e.rm % 2 != 0 || e.max_cout)) return AST_E_UNSUPPORTED;
   if (e.max_cout && cout > e.max_cout) return AST_E_UNSUPPORTED;

@@ -21,7 +21,7 @@ for f in cc:
         if filt and filt not in r["Kernel_Name"]:
             continue
         ctr[r["Dispatch_Id"]][r["Counter_Name"]] = ctr[r["Dispatch_Id"]].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-        names[r["Dispatch_Id"]] = r["Kernel_Name"].split("(")[0][-70:]
+        names[r["Dispatch_Id"]] = r["Kernel_Name"].replace("(anonymous namespace)::", "").removeprefix("void ").split("(")[0][-70:]
 rows = []
 for did, c in ctr.items():
     t = dur.get(did)

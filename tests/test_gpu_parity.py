@@ -100,6 +100,36 @@ def test_conv3x3_all_configs(case, hip_device):
     assert tried >= 1
 
 
+PERSIST_CASES = [
+    # n, cin, h, w, cout, up, pad, pool: several blocks per workgroup slot for every config 32-35
+    (4, 40, 130, 200, 192, 1, "zeros", True),   # partial last K chunk, ragged tiles, 3 channel groups
+    (8, 32, 64, 100, 64, 2, "reflect", False),  # upsampled
+    (3, 64, 66, 72, 128, 1, "reflect", True),   # blocks per slot not a whole number
+]
+
+
+@pytest.mark.parametrize("case", PERSIST_CASES)
+def test_conv3x3_persistent_bit_identical(case, hip_device):
+    """Configs 32-35 (one workgroup per CU slot walking its blocks, next block's first chunk loaded
+    under the current epilogue) against their one-block-per-workgroup forms 28-31: same k order and
+    rounding per block, so the outputs are bit-identical, and repeated launches agree."""
+    n, cin, h, w, cout, up, pad, pool = case
+    x = torch.from_numpy(synth.image(700 + cin, (n, cin, h, w)) * 2 - 0.5).to(hip_device)
+    wt = torch.from_numpy(synth.conv_weight(710 + cin, cout, cin, 3)).to(hip_device)
+    bd = torch.from_numpy(synth.conv_bias(720 + cin, cout)).to(hip_device)
+    wp = ops.pack_conv3x3(wt)
+    for cfg in (28, 29, 30, 31):
+        ref = ops.conv3x3(x, wp, bd, cout, upsample=up, pad_mode=pad, want_pre=True, want_act=True, want_pool=pool,
+                          cfg=cfg)
+        for _ in range(2):
+            got = ops.conv3x3(x, wp, bd, cout, upsample=up, pad_mode=pad, want_pre=True, want_act=True,
+                              want_pool=pool, cfg=cfg + 4)
+            torch.cuda.synchronize()
+            for r, g in zip(ref, got):
+                if r is not None:
+                    assert torch.equal(r, g), (cfg + 4, (r - g).abs().max().item())
+
+
 @pytest.mark.parametrize("cin", [1, 2, 3, 4])
 def test_conv3x3_direct_cin_le4_lds_weights(cin, hip_device):
     """The direct cin <= 4 kernel (configs 18-23) on every cin it takes, with a 192-channel weight
