@@ -337,6 +337,18 @@ class FlatFolderDataset(data.Dataset):
                 print("e:", e)
                 idx = torch.randint(0, len(paths), ())
 
+    def _decode(self, paths):
+        """The host half of _get_item: a random image of `paths` decoded to a uint8 RGB HWC array
+        (what a DataLoader worker returns; the device half is the transform, in the trainer process)."""
+        import numpy as np
+        idx = torch.randint(0, len(paths), ())
+        while True:
+            try:
+                return np.asarray(Image.open(str(paths[idx])).convert("RGB"))
+            except Exception as e:  # as _get_item: retry another image
+                print("e:", e)
+                idx = torch.randint(0, len(paths), ())
+
     def __getitem__(self, idx):
         return self._get_item(self.content_paths), self._get_item(self.style_paths)
 
@@ -360,3 +372,64 @@ class FlatFolderDatasetAE(FlatFolderDataset):
 
     def __len__(self):
         return len(self.content_paths)
+
+
+# ------------------------------------------------------------------------------------------------
+# Parallel host decoding (the reference's DataLoader(num_workers=4 | 8), train.py:66-75,
+# train_autoencoder.py:188-195): worker processes open and decode images (PIL, CPU only); the
+# trainer process uploads them and runs ToTensor and every augmentation as HIP kernels, so the GPU is
+# used by one process only. Workers are forked: build the iterator before the process touches the
+# GPU (the helpers below start their workers at once), as the reference builds its loaders first.
+# ------------------------------------------------------------------------------------------------
+
+class HostDecoded(data.Dataset):
+    """DataLoader-worker view of a FlatFolderDataset / FlatFolderDatasetAE: item = decoded uint8
+    arrays, a (content, style) pair or a content image, drawn at random as the dataset's own
+    __getitem__ does (data_loader.py:184-197, :221-233)."""
+
+    def __init__(self, dataset):
+        self.ds = dataset
+
+    def __getitem__(self, idx):
+        if isinstance(self.ds, FlatFolderDatasetAE):
+            return self.ds._decode(self.ds.content_paths)
+        return self.ds._decode(self.ds.content_paths), self.ds._decode(self.ds.style_paths)
+
+    def __len__(self):
+        return len(self.ds)
+
+
+def _collate_list(batch):
+    return batch
+
+
+def device_batches(decoded_iter, transform, pairs=True):
+    """Batches of the device transform over decoded items: (content, style) stacked [B, 3, H, W]
+    pairs, or content batches. ImageTransform keeps one output size for 2 * batch_size images,
+    so a batch stacks (data_loader.py:87-107)."""
+    for items in decoded_iter:
+        if pairs:
+            yield (torch.stack([transform(c).float() for c, _ in items]),
+                   torch.stack([transform(st).float() for _, st in items]))
+        else:
+            yield torch.stack([transform(c).float() for c in items])
+
+
+def _decoded_loader(dataset, batch_size, num_workers):
+    loader = data.DataLoader(HostDecoded(dataset), batch_size=batch_size, sampler=InfiniteSamplerWrapper(dataset),
+                             num_workers=num_workers, collate_fn=_collate_list,
+                             persistent_workers=num_workers > 0, prefetch_factor=2 if num_workers > 0 else None)
+    return iter(loader)   # starts the workers now (before the caller touches the GPU)
+
+
+def content_style_iter(content_dir, style_dir, transform, batch_size, num_workers=4):
+    """train.py:66-75: an endless iterator of (content, style) device batches, decoded by
+    `num_workers` host processes and transformed on the device (transform: e.g. ImageTransform)."""
+    ds = FlatFolderDataset(content_dir, style_dir, transform=None)
+    return device_batches(_decoded_loader(ds, batch_size, num_workers), transform, pairs=True)
+
+
+def content_iter(content_dir, transform, batch_size, num_workers=8):
+    """train_autoencoder.py:188-195: the AutoEncoder trainer's content batches, likewise."""
+    ds = FlatFolderDatasetAE(content_dir, transform=None)
+    return device_batches(_decoded_loader(ds, batch_size, num_workers), transform, pairs=False)
