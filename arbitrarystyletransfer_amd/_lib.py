@@ -69,6 +69,7 @@ SIGNATURES = {
     "ast_mb_se_fold": (_i, [_i, _p, _i, _i, _ll, _p, _p, _i, _p, _p, _p, _i, _i, _i, _p, _p]),
     "ast_mb_pw": (_i, [_i, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _i, _i, _p, _i, _p, _p]),
     "ast_mb_expand_gemm": (_i, [_i, _p, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p]),
+    "ast_mb_fold_bn_f32": (_i, [_p, _i, _i, _p, _p, _p, _p, ctypes.c_float, _i, _p, _i, _i, _p, _p]),
     "ast_mb_expand_dw_pw_supported": (_i, [_i] * 11),
     "ast_mb_expand_dw_pw": (_i, [_i, _p, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p, _i, _p, _i, _i, _i, _p, _p, _p, _p]),
     "ast_mb_conv3x3_dense": (_i, [_i, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),

@@ -1752,6 +1752,37 @@ int ed_dispatch(int dtype, EdArgs a, int k, int stride, int up, hipStream_t st) 
 }
 }  // namespace
 
+// Eval-mode BatchNorm folded into the preceding conv (mobilenetv2.py DepthWiseConv, the planned
+// inference path): s = gamma / sqrt(var + eps), w' = w * s per output row, b' = beta - mean * s --
+// the same operations and roundings as the torch expression it replaces (add, sqrt, div, mul; mean * s
+// rounded before the subtraction), one launch instead of six elementwise ones per conv, written
+// straight into the padded [rows_out][ld] layout the kernels read (padding zero).
+__global__ void fold_bn_kernel(const float* __restrict__ w, int cout, int k, const float* __restrict__ gamma,
+                               const float* __restrict__ beta, const float* __restrict__ mean,
+                               const float* __restrict__ var, float eps, int has_bn, float* __restrict__ w_out,
+                               int ld, int rows_out, float* __restrict__ b_out) {
+#pragma clang fp contract(off)  // mean * s rounded before the subtraction, as torch's two kernels
+  const int64_t total = (int64_t)rows_out * ld;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(e / ld), c = (int)(e - (int64_t)r * ld);
+    float v = 0.f;
+    if (r < cout && c < k) {
+      v = w[(int64_t)r * k + c];
+      if (has_bn) v = v * (gamma[r] / __builtin_sqrtf(var[r] + eps));
+    }
+    w_out[e] = v;
+    if (c == 0 && b_out && r < cout) {
+      float b = 0.f;
+      if (has_bn) {
+        const float sc = gamma[r] / __builtin_sqrtf(var[r] + eps);
+        const float ms = mean[r] * sc;
+        b = beta[r] - ms;
+      }
+      b_out[r] = b;
+    }
+  }
+}
+
 extern "C" {
 
 long long ast_mb_expand_dw_workspace_floats(int dtype, int has_x2, int c1, int n, int cin, int h, int w, int up,
@@ -1912,6 +1943,18 @@ int ast_adain_bf16(const void* content, const void* style, void* out, int n, int
   hipLaunchKernelGGL(adain_bf16_kernel, dim3((unsigned)((int64_t)n * c)), dim3(kThreads), 0, (hipStream_t)stream,
                      reinterpret_cast<const bf16*>(content), reinterpret_cast<const bf16*>(style),
                      reinterpret_cast<bf16*>(out), (int64_t)hc * wc, (int64_t)hs * ws, a, b, swap_style_stats ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int ast_mb_fold_bn_f32(const float* w, int cout, int k, const float* gamma, const float* beta, const float* mean,
+                       const float* var, float eps, int has_bn, float* w_out, int ld, int rows_out, float* b_out,
+                       void* stream) {
+  if (!w || !w_out || (has_bn && (!gamma || !beta || !mean || !var))) return AST_E_NULLPTR;
+  if (cout <= 0 || k <= 0 || ld < k || rows_out < cout) return AST_E_SHAPE;
+  const int64_t total = (int64_t)rows_out * ld;
+  const int blocks = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+  hipLaunchKernelGGL(fold_bn_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, cout, k, gamma, beta, mean,
+                     var, eps, has_bn, w_out, ld, rows_out, b_out);
   return (int)hipGetLastError();
 }
 

@@ -230,6 +230,28 @@ class DepthWiseConv(nn.Module):
         s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
         return w * s.view(-1, 1, 1, 1), bn.bias.detach().float() - bn.running_mean.detach().float() * s
 
+    def _fold_into(self, i, rows, ld, want_bias):
+        """_fold of conv _layers[i] as one HIP launch (ast_mb_fold_bn_f32: the same roundings),
+        into a zero-padded [rows][ld] fp32 buffer; the bias (zeros without a BatchNorm) or None."""
+        conv = self._layers[i]
+        bn = self._layers[i + 1] if i + 1 < len(self._layers) else None
+        has_bn = isinstance(bn, nn.BatchNorm2d)
+        w = conv.weight.detach()
+        if w.dtype != torch.float32 or not w.is_contiguous():
+            w = w.float().contiguous()
+        cout, k = int(w.shape[0]), int(w[0].numel())
+        out = torch.empty((rows, ld), device=w.device, dtype=torch.float32)
+        b = torch.empty(cout, device=w.device, dtype=torch.float32) if (want_bias or has_bn) else None
+        args = [None] * 4
+        if has_bn:
+            args = [t.detach() if t.dtype == torch.float32 else t.detach().float()
+                    for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var)]
+            args = [t if t.is_contiguous() else t.contiguous() for t in args]
+        check(lib().ast_mb_fold_bn_f32(ptr(w), cout, k, *(ptr(t) for t in args), float(bn.eps) if has_bn else 0.0,
+                                       int(has_bn), ptr(out), ld, rows, ptr(b), stream_ptr(w.device)),
+              "fold BatchNorm")
+        return out, b
+
     def _plan(self, dt, device) -> _BlockPlan:
         stamp = _stamp(self, dt, device)
         if getattr(self, "_plan_stamp", None) == stamp:
@@ -244,24 +266,18 @@ class DepthWiseConv(nn.Module):
             p.cin_pad = 0
         else:
             i_pw1, i_dw, i_pw = convs
-            w1, b1 = self._fold(i_pw1)
             p.cin_pad = _round_up(self.inp, 16 if dt == torch.bfloat16 else 4)
-            w1p = torch.zeros((_round_up(hid, 16), p.cin_pad), device=device, dtype=torch.float32)
-            w1p[:hid, :self.inp] = w1.view(hid, self.inp)
-            p.w1p = w1p.to(dt).contiguous()
-            p.b1 = (b1 if b1 is not None else torch.zeros(hid, device=device)).contiguous()
-        wd, bd = self._fold(i_dw)
-        p.wd = wd.reshape(hid, -1).contiguous()
-        p.bd = (bd if bd is not None else torch.zeros(hid, device=device)).contiguous()
+            w1p, p.b1 = self._fold_into(i_pw1, _round_up(hid, 16), p.cin_pad, True)
+            p.w1p = w1p if dt == torch.float32 else w1p.to(dt).contiguous()
+        k2 = self._layers[i_dw].weight[0].numel()
+        p.wd, p.bd = self._fold_into(i_dw, hid, k2, True)
         fc1, fc2 = se.fc[0], se.fc[2]
         p.fc1w = fc1.weight.detach().float().contiguous()
         p.fc1b = fc1.bias.detach().float().contiguous()
         p.fc2w = fc2.weight.detach().float().contiguous()
         p.fc2b = fc2.bias.detach().float().contiguous()
         p.red = fc1.out_features
-        w2, b2 = self._fold(i_pw)
-        p.w2 = w2.view(cout, hid).contiguous()
-        p.b2 = b2.contiguous() if b2 is not None else None
+        p.w2, p.b2 = self._fold_into(i_pw, cout, hid, False)
         p.hid_pad = _round_up(hid, 32)
         p.cout_pad = _round_up(cout, 16)
         self._pl, self._plan_stamp = p, stamp

@@ -350,6 +350,15 @@ int ast_mb_pw(int dtype, const void* d, int n, int hid, int hid_pad, int h, int 
 int ast_mb_expand_gemm(int dtype, const void* x1, const void* x2, int c1, int n, int cin, int h, int w,
                        const void* w1p, const float* b1, int hid, int cin_pad, void* out, void* stream);
 
+/* Eval-mode BatchNorm folded into the conv before it (mobilenetv2.py:223-231 _fold, the planned
+ * inference path of DepthWiseConv; reference layers mobilenetv2.py:146-160): w is [cout][k],
+ * s = gamma / sqrt(var + eps), w_out[r][c] = w[r][c] * s[r] for r < cout, c < k and 0 in the padding
+ * of the [rows_out][ld] output; b_out[r] = beta[r] - mean[r] * s[r] (NULL: not written). has_bn 0:
+ * a padded copy and a zero bias. Same roundings as the torch expression. */
+int ast_mb_fold_bn_f32(const float* w, int cout, int k, const float* gamma, const float* beta, const float* mean,
+                       const float* var, float eps, int has_bn, float* w_out, int ld, int rows_out, float* b_out,
+                       void* stream);
+
 /* Dense 3x3 reflect-pad convs of the variant: block 0 (conv_3x3_bn, mobilenetv2.py:38-43:
  * cin 3 -> cout 16, no bias, act 1 = Hardswish, fp32 input) and the decoder output conv
  * (models.py:300-316: cin 16 -> cout 3 + bias, fp32 output, act 2 = Hardtanh(0,1) when exporting,

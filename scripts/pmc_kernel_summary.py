@@ -15,7 +15,7 @@ for f in sorted(glob.glob(os.path.join(root, f"{tag}_pmc_*", "**", "*counter_col
         k = r["Kernel_Name"]
         if filt and filt not in k:
             continue
-        k = k.split("(")[0][-60:]
+        k = k.replace("(anonymous namespace)::", "").removeprefix("void ").split("(")[0][-60:]
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         cnt[k][r["Counter_Name"]] += 1
 for kk, d in agg.items():

@@ -122,6 +122,37 @@ def test_fused_pair_matches_unfused(case, hip_device, monkeypatch):
     assert rel_inf(y_f, ref) <= BF16_BLOCK_TOL
 
 
+@pytest.mark.parametrize("norm,k", [(True, 3), (True, 5), (False, 3)])
+def test_plan_fold_kernel_matches_torch_fold(norm, k, hip_device):
+    """The block plan's BatchNorm fold (ast_mb_fold_bn_f32, one launch per conv) is bit-identical to
+    the torch expression it replaces (DepthWiseConv._fold: add, sqrt, div, mul, mul, sub), with
+    non-trivial running statistics, and zero in the padding of the expand weights."""
+    blk = synth.live_init_(DepthWiseConv(20, 24, 1, 6, kernel_size=k, use_norm=norm), 990 + k)
+    g = torch.Generator().manual_seed(3)
+    with torch.no_grad():
+        for m in blk.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.copy_(torch.randn(m.num_features, generator=g))
+                m.running_var.copy_(torch.rand(m.num_features, generator=g) * 2 + 0.05)
+                m.weight.copy_(torch.randn(m.num_features, generator=g))
+                m.bias.copy_(torch.randn(m.num_features, generator=g))
+    blk = blk.eval().to(hip_device)
+    p = blk._plan(torch.float32, hip_device)
+    convs = [i for i, m in enumerate(blk._layers) if isinstance(m, torch.nn.Conv2d)]
+    hid = blk.hidden_dim
+    w1, b1 = blk._fold(convs[0])
+    assert torch.equal(p.w1p[:hid, :20], w1.view(hid, 20))
+    assert torch.count_nonzero(p.w1p[:, 20:]) == 0 and torch.count_nonzero(p.w1p[hid:]) == 0
+    wd, bd = blk._fold(convs[1])
+    assert torch.equal(p.wd, wd.reshape(hid, -1))
+    w2, b2 = blk._fold(convs[2])
+    assert torch.equal(p.w2, w2.view(24, hid))
+    if norm:
+        assert torch.equal(p.b1, b1) and torch.equal(p.bd, bd) and torch.equal(p.b2, b2)
+    else:
+        assert torch.count_nonzero(p.b1) == 0 and torch.count_nonzero(p.bd) == 0 and p.b2 is None
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_ada_out_split_input_matches_cat(dtype, hip_device):
     blk = synth.live_init_(DepthWiseConv(256, 128, 1, 3, use_norm=False, use_identity=False), 7)
