@@ -506,6 +506,10 @@ __global__ void pack_x3_kernel(const float* __restrict__ wp, bf16* __restrict__ 
   }
 }
 
+#ifndef X3_HS_PAD
+#define X3_HS_PAD 1
+#endif
+
 template <int WM, int RM, int RN, int UP>
 struct X3Cfg {
   static constexpr int NT = WM * 64;
@@ -513,11 +517,17 @@ struct X3Cfg {
   static constexpr int BN = RN * 32;                 // output channels per tile
   static constexpr int SR = TH / UP + 2;             // source rows incl. halo
   static constexpr int SC = TW / UP + 2;             // source columns incl. halo
-  static constexpr int A_PLANE = 2 * SR * SC;        // 16-B units per plane
+  static constexpr int A_ITEMS = 2 * SR * SC;        // gather items: 16-B units of 8 channels, both halves
+  // 16-B units per 8-channel half, padded to a multiple of 16 units (64 banks): the M16 A operand
+  // reads both halves (and two planes) in one ds_read_b128, whose lane groups {0-3,12-15,20-27} /
+  // {4-11,16-19,28-31} mix the halves -- unpadded (612 units = 16 banks apart) they collide on 16
+  // banks per group (2-way, profiles/r04p: 22% of the LDS cycles were conflicts)
+  static constexpr int HS = X3_HS_PAD ? (SR * SC + 15) / 16 * 16 : SR * SC;
+  static constexpr int A_PLANE = 2 * HS;             // 16-B units per plane
   static constexpr int A_UNITS = 3 * A_PLANE;
   static constexpr int B_ROWS = 3 * 9 * 2;           // (plane, tap, h)
   static constexpr int B_UNITS = B_ROWS * BN;
-  static constexpr int A_T = (A_PLANE + NT - 1) / NT;  // gather items per thread (one item = 8 channels)
+  static constexpr int A_T = (A_ITEMS + NT - 1) / NT;  // gather items per thread (one item = 8 channels)
   static constexpr int B_T = (B_UNITS + NT - 1) / NT;
   static constexpr int NS = UP == 1 ? RM + 2 : RM / 2 + 2;  // source rows a wave's RM output rows read
   static constexpr int LDS_TILES = (A_UNITS + B_UNITS) * 16;
@@ -631,6 +641,7 @@ template <int WM, int RM, int RN, int UP, int OCC, bool M16 = false>
 __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   using C = X3Cfg<WM, RM, RN, UP>;
   constexpr int NT = C::NT, TH = C::TH, BN = C::BN, SR = C::SR, SC = C::SC, A_PLANE = C::A_PLANE;
+  constexpr int HS = C::HS, A_ITEMS = C::A_ITEMS;
   constexpr int A_T = C::A_T, B_T = C::B_T, NS = C::NS;
   static_assert(RM % 2 == 0, "even rows per wave (pool windows, upsample row pairs)");
   extern __shared__ __attribute__((aligned(16))) u32x4 x3_smem[];
@@ -664,13 +675,13 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   bool g_ok[A_T];
 #pragma unroll
   for (int i = 0; i < A_T; ++i) {
-    const int e = min(tid + i * NT, A_PLANE - 1);
+    const int e = min(tid + i * NT, A_ITEMS - 1);
     const int c = e % SC, rest = e / SC, r = rest % SR, hh = rest / SR;
     const int sy = src_index<UP>(sy0 + r, Hin, a.reflect), sx = src_index<UP>(sx0 - 1 + c, Win, a.reflect);
     g_ok[i] = sy >= 0 && sx >= 0;
     g_pix[i] = (unsigned)(max(sy, 0) * Win + max(sx, 0));
     g_off[i] = g_ok[i] ? 4u * (unsigned)(8 * hh * plane_in) + 4u * g_pix[i] : 0x7ffffff0u;
-    g_lds[i] = e;
+    g_lds[i] = hh * HS + r * SC + c;
     g_h[i] = hh;
   }
   const int plane_b = 4 * plane_in;
@@ -706,7 +717,7 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
 #define X3_STORE(KC)                                                                                    \
   {                                                                                                     \
     _Pragma("unroll") for (int i = 0; i < A_T; ++i) {                                                   \
-      if (tid + i * NT < A_PLANE) {                                                                     \
+      if (tid + i * NT < A_ITEMS) {                                                                     \
         if ((KC) * kX3K + kX3K > a.Cin) { /* partial last chunk: padding and channels past Cin */        \
           const int cn = a.Cin - (KC) * kX3K - 8 * g_h[i];                                              \
           _Pragma("unroll") for (int j = 0; j < 8; ++j) ra[i][j] = (g_ok[i] && j < cn) ? ra[i][j] : 0.f; \
@@ -783,7 +794,7 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
           }
 #pragma unroll
           for (int i = 0; i < RM; ++i) {
-            const int srow = (hh16 * SR + srow0 + x3_srel<UP>(i, ky)) * SC;
+            const int srow = hh16 * HS + (srow0 + x3_srel<UP>(i, ky)) * SC;
             bf16x8 f1[2], f2[2];
 #pragma unroll
             for (int pt = 0; pt < 2; ++pt) {
@@ -818,7 +829,7 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
           bf16x8 af[3];
 #pragma unroll
           for (int p = 0; p < 3; ++p)
-            af[p] = __builtin_bit_cast(bf16x8, As[p * A_PLANE + (h * SR + srow0 + s) * SC + acol[kx]]);
+            af[p] = __builtin_bit_cast(bf16x8, As[p * A_PLANE + h * HS + (srow0 + s) * SC + acol[kx]]);
 #pragma unroll
           for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -921,6 +932,7 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3p_kernel(ConvArgs, int
 #define A_ x3p_args()
   using C = X3Cfg<WM, RM, RN, UP>;
   constexpr int NT = C::NT, TH = C::TH, BN = C::BN, SR = C::SR, SC = C::SC, A_PLANE = C::A_PLANE;
+  constexpr int HS = C::HS, A_ITEMS = C::A_ITEMS;
   constexpr int A_T = C::A_T, B_T = C::B_T;
   constexpr int Q = 2 * RN;
   static_assert(RM % 2 == 0, "even rows per wave (pool windows, upsample row pairs)");
@@ -961,13 +973,13 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3p_kernel(ConvArgs, int
     int tv_ = tid; /* laundered: the per-thread item decode is redone here, not hoisted and spilled */ \
     asm volatile("" : "+v"(tv_));                                                                   \
     _Pragma("unroll") for (int i = 0; i < A_T; ++i) {                                               \
-      const int e = min(tv_ + i * NT, A_PLANE - 1);                                                 \
+      const int e = min(tv_ + i * NT, A_ITEMS - 1);                                                 \
       const int c = e % SC, rest = e / SC, r = rest % SR, hh = rest / SR;                           \
       const int sy = src_index<UP>(sy0_ + r, Hin, A_.reflect), sx = src_index<UP>(sx0_ - 1 + c, Win, A_.reflect); \
       g_ok[i] = sy >= 0 && sx >= 0;                                                                 \
       g_pix[i] = (unsigned)(max(sy, 0) * Win + max(sx, 0));                                         \
       g_off[i] = g_ok[i] ? 4u * (unsigned)(8 * hh * plane_in) + 4u * g_pix[i] : 0x7ffffff0u;        \
-      g_lds[i] = e;                                                                                 \
+      g_lds[i] = hh * HS + r * SC + c;                                                              \
       g_h[i] = hh;                                                                                  \
     }                                                                                               \
     _Pragma("unroll") for (int i = 0; i < B_T; ++i) {                                               \
@@ -1002,7 +1014,7 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3p_kernel(ConvArgs, int
   {                                                                                                     \
     const ConvArgs& ka_ = x3p_args(); /* one laundered argument pointer per expansion */                \
     _Pragma("unroll") for (int i = 0; i < A_T; ++i) {                                                   \
-      if (tid + i * NT < A_PLANE) {                                                                     \
+      if (tid + i * NT < A_ITEMS) {                                                                     \
         if ((KC) * kX3K + kX3K > ka_.Cin) {                                                               \
           const int cn = ka_.Cin - (KC) * kX3K - 8 * g_h[i];                                              \
           _Pragma("unroll") for (int j = 0; j < 8; ++j) ra[i][j] = (g_ok[i] && j < cn) ? ra[i][j] : 0.f; \
@@ -1074,7 +1086,7 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3p_kernel(ConvArgs, int
           }
 #pragma unroll
           for (int i = 0; i < RM; ++i) {
-            const int srow = (mhh16 * SR + srow0 + x3_srel<UP>(i, ky)) * SC;
+            const int srow = mhh16 * HS + (srow0 + x3_srel<UP>(i, ky)) * SC;
             bf16x8 f1[2], f2[2];
 #pragma unroll
             for (int pt = 0; pt < 2; ++pt) {
