@@ -801,15 +801,23 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
               f1[pt] = __builtin_bit_cast(bf16x8, As[apl1 + srow + acol16[pt][kx]]);
               f2[pt] = __builtin_bit_cast(bf16x8, As[apl2 + srow + acol16[pt][kx]]);
             }
+            // the three products of an accumulator in the same order, but product-major: 2Q
+            // independent MFMAs separate each from the next one on the same accumulator
 #pragma unroll
             for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
-              for (int q = 0; q < Q; ++q) {
-                f32x4v c = acc16[i][pt][q];
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g3[q], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[pt], g2[q], c, 0, 0, 0);
-                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g1[q], c, 0, 0, 0);
-              }
+              for (int q = 0; q < Q; ++q)
+                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g3[q], acc16[i][pt][q], 0, 0, 0);
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+              for (int q = 0; q < Q; ++q)
+                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[pt], g2[q], acc16[i][pt][q], 0, 0, 0);
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+              for (int q = 0; q < Q; ++q)
+                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g1[q], acc16[i][pt][q], 0, 0, 0);
           }
         }
       }
@@ -1093,15 +1101,23 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3p_kernel(ConvArgs, int
               f1[pt] = __builtin_bit_cast(bf16x8, As[apl1 + srow + acol16[pt][kx]]);
               f2[pt] = __builtin_bit_cast(bf16x8, As[apl2 + srow + acol16[pt][kx]]);
             }
+            // the three products of an accumulator in the same order, but product-major: 2Q
+            // independent MFMAs separate each from the next one on the same accumulator
 #pragma unroll
             for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
-              for (int q = 0; q < Q; ++q) {
-                f32x4v c = acc16[i][pt][q];
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g3[q], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[pt], g2[q], c, 0, 0, 0);
-                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g1[q], c, 0, 0, 0);
-              }
+              for (int q = 0; q < Q; ++q)
+                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g3[q], acc16[i][pt][q], 0, 0, 0);
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+              for (int q = 0; q < Q; ++q)
+                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[pt], g2[q], acc16[i][pt][q], 0, 0, 0);
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+              for (int q = 0; q < Q; ++q)
+                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g1[q], acc16[i][pt][q], 0, 0, 0);
           }
         }
       }
