@@ -678,24 +678,35 @@ __global__ __launch_bounds__(64 * (NCB + 1)) __attribute__((amdgpu_waves_per_eu(
           }
         }
         const bf16* img = dimg[orow & 1];
+        // k-major over the NT tiles: each tile's k-steps in the same order (bit-identical), NT - 1
+        // independent MFMAs between consecutive ones on one accumulator, and each image fragment
+        // read once per k-step for both output-channel tiles
+        f32x4 acc[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const int col = (t & 1) * 16 + 4 * p4;
-          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int kc = 0; kc < (EDPW_T_NOGEMM ? 0 : EDPW_T_GEMM1 ? 1 : NCB); ++kc) {
-            const s16x4 alo = afr[t / 2][kc][0];
-            const s16x4 ahi = afr[t / 2][kc][1];
+        for (int kc = 0; kc < (EDPW_T_NOGEMM ? 0 : EDPW_T_GEMM1 ? 1 : NCB); ++kc) {
+          bf16x8 bfr[2];
+#pragma unroll
+          for (int ph = 0; ph < 2; ++ph) {
+            const int col = ph * 16 + 4 * p4;
             const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (32 * kc + 4 * g + q4) * DP + col));
             const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (32 * kc + 16 + 4 * g + q4) * DP + col));
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8, __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7)),
-                __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7)), acc, 0, 0, 0);
+            bfr[ph] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
           }
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, __builtin_shufflevector(afr[t / 2][kc][0], afr[t / 2][kc][1], 0, 1, 2, 3, 4, 5,
+                                                                   6, 7)),
+                bfr[t & 1], acc[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
           const int px = (t & 1) * 16 + (lane & 15);
           if (px >= 2 && px < 2 + OW) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) ostg[(t / 2 * 16 + 4 * g + j) * 32 + px - 2] = acc[j] + bco[t / 2][j];
+            for (int j = 0; j < 4; ++j) ostg[(t / 2 * 16 + 4 * g + j) * 32 + px - 2] = acc[t][j] + bco[t / 2][j];
           }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes are done
