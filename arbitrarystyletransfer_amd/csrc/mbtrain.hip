@@ -183,7 +183,13 @@ __global__ __launch_bounds__(kT) void gemm_kernel(GemmArgs a) {
 // (profiles/r03_gemm_probe.txt). Wave w owns columns 64w .. 64w + 63 and all 64 rows (2 x 2
 // accumulators of 32 x 32; the second row block is skipped when M <= 32); K in chunks of 16 with
 // the next chunk's loads in flight during the MFMAs. Same products and k order as gemm_kernel.
-constexpr int WGN = 256, WGK = 16;
+#ifndef WGW_K
+#define WGW_K 16  // k rows per chunk (32 and 64 measured slower: profiles/r04_gemm_wide_variants.txt)
+#endif
+constexpr int WGN = 256, WGK = WGW_K;
+#ifndef WGW_T_NOSTORE
+#define WGW_T_NOSTORE 0  // timing builds: gemm_wide_kernel without its C stores (wrong results)
+#endif
 
 __global__ __launch_bounds__(kT) void gemm_wide_kernel(GemmArgs a, int P) {
   __shared__ float As[WGK][GT + 4];   // [k][m]
@@ -198,19 +204,19 @@ __global__ __launch_bounds__(kT) void gemm_wide_kernel(GemmArgs a, int P) {
   const bool nv = nq < a.N;  // a quad never straddles images (P % 4 == 0, N % 4 == 0)
   const int img = nv ? nq / P : 0;
   const float* bbase = a.B + (int64_t)img * a.sBb + (nq - img * P);
-  const int am = tid >> 2, ak = 4 * (tid & 3);
+  const int am = tid >> 2, ak = (WGK / 4) * (tid & 3);
   const bool amv = m0 + am < a.M;
   const float* abase = a.A + (int64_t)(m0 + am) * a.sAm;
-  float4 rb[4];
-  float ra[4];
+  float4 rb[WGK / 4];
+  float ra[WGK / 4];
   auto load = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < WGK / 4; ++i) {
       const int k = k0 + kr0 + 4 * i;
       rb[i] = (nv && k < a.K) ? *reinterpret_cast<const float4*>(bbase + (int64_t)k * a.sBk) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < WGK / 4; ++j) {
       const int k = k0 + ak + j;
       ra[j] = (amv && k < a.K) ? abase[(int64_t)k * a.sAk] : 0.f;
     }
@@ -223,9 +229,9 @@ __global__ __launch_bounds__(kT) void gemm_wide_kernel(GemmArgs a, int P) {
   load(0);
   for (int k0 = 0; k0 < a.K; k0 += WGK) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(&Bs[kr0 + 4 * i][4 * qn]) = rb[i];
+    for (int i = 0; i < WGK / 4; ++i) *reinterpret_cast<float4*>(&Bs[kr0 + 4 * i][4 * qn]) = rb[i];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) As[ak + j][am] = ra[j];
+    for (int j = 0; j < WGK / 4; ++j) As[ak + j][am] = ra[j];
     __syncthreads();
     if (k0 + WGK < a.K) load(k0 + WGK);
 #pragma unroll
@@ -253,7 +259,7 @@ __global__ __launch_bounds__(kT) void gemm_wide_kernel(GemmArgs a, int P) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int m = m0 + 32 * mi + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (m < a.M) {
+        if (m < a.M && (!WGW_T_NOSTORE || acc[mi][ni][i] == 1.2345e-30f)) {
           float* c = cc + (int64_t)m * a.sCm;
           *c = a.accumulate ? *c + acc[mi][ni][i] : acc[mi][ni][i];
         }
