@@ -827,9 +827,33 @@ __global__ __launch_bounds__(kT) void plane_dot_kernel(const float* __restrict__
   const float* xp = x + p * hw;
   const float* yp = y ? y + p * hw : nullptr;
   float s = 0.f;
-  for (int64_t i = threadIdx.x; i < hw; i += kT) {
-    if (yp) s += xp[i] * (ACT ? elt<0>(yp[i], 0.f) : yp[i]);
-    else s += ACT ? elt<0>(xp[i], 0.f) : xp[i];
+  if ((hw & 3) == 0 && ((uintptr_t)xp & 15) == 0 && (!yp || ((uintptr_t)yp & 15) == 0)) {
+    // 16-byte loads, four independent partial sums per thread (a fixed order: deterministic); the
+    // scalar loop below issued 4x the loads, each sum one dependent chain
+    const float4* x4 = reinterpret_cast<const float4*>(xp);
+    const float4* y4 = reinterpret_cast<const float4*>(yp);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    for (int64_t i = threadIdx.x; i < hw / 4; i += kT) {
+      const float4 a = x4[i];
+      if (yp) {
+        const float4 b = y4[i];
+        s0 += a.x * (ACT ? elt<0>(b.x, 0.f) : b.x);
+        s1 += a.y * (ACT ? elt<0>(b.y, 0.f) : b.y);
+        s2 += a.z * (ACT ? elt<0>(b.z, 0.f) : b.z);
+        s3 += a.w * (ACT ? elt<0>(b.w, 0.f) : b.w);
+      } else {
+        s0 += ACT ? elt<0>(a.x, 0.f) : a.x;
+        s1 += ACT ? elt<0>(a.y, 0.f) : a.y;
+        s2 += ACT ? elt<0>(a.z, 0.f) : a.z;
+        s3 += ACT ? elt<0>(a.w, 0.f) : a.w;
+      }
+    }
+    s = (s0 + s1) + (s2 + s3);
+  } else {
+    for (int64_t i = threadIdx.x; i < hw; i += kT) {
+      if (yp) s += xp[i] * (ACT ? elt<0>(yp[i], 0.f) : yp[i]);
+      else s += ACT ? elt<0>(xp[i], 0.f) : xp[i];
+    }
   }
   const float t = block_sum(s, sh);
   if (threadIdx.x == 0) out[p] = t * scale;
