@@ -867,11 +867,31 @@ template <int OP>
 __global__ __launch_bounds__(kT) void plane_scale_kernel(const float* __restrict__ x, const float* __restrict__ gate,
                                                          const float* __restrict__ gadd, const float* __restrict__ a,
                                                          int64_t hw, int64_t planes, float* __restrict__ y) {
+  const bool v4 = (hw & 3) == 0 && (((uintptr_t)x | (uintptr_t)y | (uintptr_t)(OP == 2 ? a : x)) & 15) == 0;
   for (int64_t p = blockIdx.y; p < planes; p += gridDim.y) {
     const float gv = gate[p], av = gadd ? gadd[p] : 0.f;
     const float* xp = x + p * hw;
     const float* ap = OP == 2 ? a + p * hw : nullptr;
     float* yp = y + p * hw;
+    if (v4) {  // the block's 4 kT elements as one 16-byte access per thread (same values)
+      const int64_t i4 = (int64_t)blockIdx.x * kT + threadIdx.x;
+      if (4 * i4 < hw) {
+        const float4 xv = reinterpret_cast<const float4*>(xp)[i4];
+        float4 o;
+        if (OP == 0) {
+          o = make_float4(fmaf(xv.x, gv, av), fmaf(xv.y, gv, av), fmaf(xv.z, gv, av), fmaf(xv.w, gv, av));
+        } else if (OP == 1) {
+          o = make_float4(elt<0>(xv.x, 0.f) * gv, elt<0>(xv.y, 0.f) * gv, elt<0>(xv.z, 0.f) * gv,
+                          elt<0>(xv.w, 0.f) * gv);
+        } else {
+          const float4 av4 = reinterpret_cast<const float4*>(ap)[i4];
+          o = make_float4(elt<1>(av4.x, fmaf(xv.x, gv, av)), elt<1>(av4.y, fmaf(xv.y, gv, av)),
+                          elt<1>(av4.z, fmaf(xv.z, gv, av)), elt<1>(av4.w, fmaf(xv.w, gv, av)));
+        }
+        reinterpret_cast<float4*>(yp)[i4] = o;
+      }
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t i = (int64_t)blockIdx.x * 4 * kT + j * kT + threadIdx.x;
