@@ -677,6 +677,18 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const float* __restrict__ 
     const float sc = invstd[ch] * (gamma ? gamma[ch] : 1.f), mu = mean[ch], bt = beta ? beta[ch] : 0.f;
     const float* xp = x + (int64_t)pl * hw;
     float* yp = y + (int64_t)pl * hw;
+    if ((hw & 3) == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0) {  // one 16-byte access per thread
+      const int64_t i4 = (int64_t)blockIdx.x * kT + threadIdx.x;
+      if (4 * i4 < hw) {
+        const float4 xv = reinterpret_cast<const float4*>(xp)[i4];
+        float v[4] = {bn_aff(xv.x, mu, sc, bt), bn_aff(xv.y, mu, sc, bt), bn_aff(xv.z, mu, sc, bt),
+                      bn_aff(xv.w, mu, sc, bt)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = ACT ? elt<0>(v[e], 0.f) : v[e];
+        reinterpret_cast<float4*>(yp)[i4] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t i = (int64_t)blockIdx.x * 4 * kT + j * kT + threadIdx.x;
@@ -750,6 +762,23 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restric
     const float bt = ACT && beta ? beta[ch] : 0.f;
     const float inv_m = inv_count[0], a = sdy[ch] * inv_m, bq = sdyx[ch] * inv_m;
     const int64_t base = (int64_t)pl * hw;
+    if ((hw & 3) == 0 && (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) & 15) == 0) {  // 16-byte accesses
+      const int64_t i4 = (int64_t)blockIdx.x * kT + threadIdx.x;
+      if (4 * i4 < hw) {
+        const float4 x4 = reinterpret_cast<const float4*>(x + base)[i4];
+        const float4 g4 = reinterpret_cast<const float4*>(dy + base)[i4];
+        const float xs[4] = {x4.x, x4.y, x4.z, x4.w}, gs[4] = {g4.x, g4.y, g4.z, g4.w};
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gv = ACT ? elt<1>(bn_aff(xs[e], mu, gm, bt), gs[e]) : gs[e];
+          const float xh = (xs[e] - mu) * is;
+          o[e] = gm * (gv - a - xh * bq);
+        }
+        reinterpret_cast<float4*>(dx + base)[i4] = make_float4(o[0], o[1], o[2], o[3]);
+      }
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t i = (int64_t)blockIdx.x * 4 * kT + j * kT + threadIdx.x;
