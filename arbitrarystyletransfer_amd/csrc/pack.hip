@@ -15,16 +15,20 @@ namespace {
 constexpr int kT = 256;
 
 // xp[gi][c][y][q], q = g*(w+gap) + j: image gi*G+g's pixel j (0 in gaps / missing images)
+// IDX: the index type of the element decomposition -- 32-bit when the tensor allows it (the 64-bit
+// divisions by runtime sizes cost several times the 32-bit ones, and this gather is all index math)
+template <typename IDX>
 __global__ __launch_bounds__(kT) void pack_kernel(const float* __restrict__ x, int n1, const float* __restrict__ x2,
                                                   int n, int c, int h, int w, int G, int gap, int wp,
                                                   float* __restrict__ xp, int64_t total) {
   for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
-    const int q = (int)(e % wp);
-    const int64_t r = e / wp;  // (gi*c + ch)*h + y
-    const int y = (int)(r % h);
-    const int64_t r2 = r / h;
-    const int ch = (int)(r2 % c);
-    const int gi = (int)(r2 / c);
+    const IDX ei = (IDX)e;
+    const int q = (int)(ei % (IDX)wp);
+    const IDX r = ei / (IDX)wp;  // (gi*c + ch)*h + y
+    const int y = (int)(r % (IDX)h);
+    const IDX r2 = r / (IDX)h;
+    const int ch = (int)(r2 % (IDX)c);
+    const int gi = (int)(r2 / (IDX)c);
     const int g = q / (w + gap), j = q - g * (w + gap);
     const int img = gi * G + g;
     float v = 0.f;
@@ -37,15 +41,17 @@ __global__ __launch_bounds__(kT) void pack_kernel(const float* __restrict__ x, i
 }
 
 // out[i][c][y][x] = yp[i / G][c][y][(i % G) * sp + x]
+template <typename IDX>
 __global__ __launch_bounds__(kT) void unpack_kernel(const float* __restrict__ yp, int c, int h, int w, int G, int sp,
                                                     int wp, float* __restrict__ out, int64_t total) {
   for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
-    const int xx = (int)(e % w);
-    const int64_t r = e / w;
-    const int y = (int)(r % h);
-    const int64_t r2 = r / h;
-    const int ch = (int)(r2 % c);
-    const int i = (int)(r2 / c);
+    const IDX ei = (IDX)e;
+    const int xx = (int)(ei % (IDX)w);
+    const IDX r = ei / (IDX)w;
+    const int y = (int)(r % (IDX)h);
+    const IDX r2 = r / (IDX)h;
+    const int ch = (int)(r2 % (IDX)c);
+    const int i = (int)(r2 / (IDX)c);
     out[e] = yp[(((int64_t)(i / G) * c + ch) * h + y) * wp + (i % G) * sp + xx];
   }
 }
@@ -66,8 +72,12 @@ int ast_pack_images_f32(const float* x, int n1, const float* x2, int n2, int c, 
   const int n = n1 + n2, ng = (n + G - 1) / G;
   const int wp = G * (w + gap) - gap;
   const int64_t total = (int64_t)ng * c * h * wp;
-  hipLaunchKernelGGL(pack_kernel, dim3(grid_for(total)), dim3(kT), 0, (hipStream_t)stream, x, n1, x2, n, c, h, w, G,
-                     gap, wp, xp, total);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL(pack_kernel<unsigned>, dim3(grid_for(total)), dim3(kT), 0, (hipStream_t)stream, x, n1, x2, n, c,
+                       h, w, G, gap, wp, xp, total);
+  else
+    hipLaunchKernelGGL(pack_kernel<int64_t>, dim3(grid_for(total)), dim3(kT), 0, (hipStream_t)stream, x, n1, x2, n, c,
+                       h, w, G, gap, wp, xp, total);
   return (int)hipGetLastError();
 }
 
@@ -76,8 +86,12 @@ int ast_unpack_images_f32(const float* yp, int n, int c, int h, int w, int G, in
   if (!yp || !out) return AST_E_NULLPTR;
   if (n <= 0 || c <= 0 || h <= 0 || w <= 0 || G <= 0 || sp < w || (G - 1) * sp + w > wp) return AST_E_SHAPE;
   const int64_t total = (int64_t)n * c * h * w;
-  hipLaunchKernelGGL(unpack_kernel, dim3(grid_for(total)), dim3(kT), 0, (hipStream_t)stream, yp, c, h, w, G, sp, wp,
-                     out, total);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL(unpack_kernel<unsigned>, dim3(grid_for(total)), dim3(kT), 0, (hipStream_t)stream, yp, c, h, w, G,
+                       sp, wp, out, total);
+  else
+    hipLaunchKernelGGL(unpack_kernel<int64_t>, dim3(grid_for(total)), dim3(kT), 0, (hipStream_t)stream, yp, c, h, w, G,
+                       sp, wp, out, total);
   return (int)hipGetLastError();
 }
 
