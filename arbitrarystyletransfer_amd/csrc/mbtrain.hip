@@ -277,6 +277,14 @@ __global__ __launch_bounds__(kT) void gemm_reduce_kernel(GemmArgs a, int zper) {
     const float* p = a.part + (int64_t)cb * zper * mn + e;
     float s = 0.f;
     int z = 0;
+    // 16 loads in flight per thread, added in z order (the grid is small: mn is a weight's size)
+    for (; z + 16 <= zper; z += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = p[(int64_t)(z + u) * mn];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
     for (; z + 4 <= zper; z += 4) {
       const float v0 = p[(int64_t)z * mn], v1 = p[(int64_t)(z + 1) * mn];
       const float v2 = p[(int64_t)(z + 2) * mn], v3 = p[(int64_t)(z + 3) * mn];
