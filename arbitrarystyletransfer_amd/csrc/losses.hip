@@ -418,12 +418,33 @@ __global__ void huber_kernel(const float* __restrict__ x, const float* __restric
   __shared__ float sh[4];
   const float c = w * inv_numel * gs(gscale);
   float s = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
-    const float d = x[i] - y[i];
-    s += huber(d);
-    if (dx) {
-      const float v = c * huber_grad(d);
-      dx[i] = accumulate ? dx[i] + v : v;
+  if ((n & 3) == 0 && (((uintptr_t)x | (uintptr_t)y | (uintptr_t)(dx ? dx : x)) & 15) == 0) {
+    // 16-byte accesses (the grid is capped for the loss commit, so each thread streams many
+    // elements: 4x fewer memory instructions); a fixed element-to-thread map, deterministic
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const float4* y4 = reinterpret_cast<const float4*>(y);
+    float4* d4 = reinterpret_cast<float4*>(dx);
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n / 4; i += (int64_t)gridDim.x * kThreads) {
+      const float4 a = x4[i], b = y4[i];
+      const float d[4] = {a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w};
+      s += (huber(d[0]) + huber(d[1])) + (huber(d[2]) + huber(d[3]));
+      if (dx) {
+        float4 v = make_float4(c * huber_grad(d[0]), c * huber_grad(d[1]), c * huber_grad(d[2]), c * huber_grad(d[3]));
+        if (accumulate) {
+          const float4 o = d4[i];
+          v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+        }
+        d4[i] = v;
+      }
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+      const float d = x[i] - y[i];
+      s += huber(d);
+      if (dx) {
+        const float v = c * huber_grad(d);
+        dx[i] = accumulate ? dx[i] + v : v;
+      }
     }
   }
   const float t = block_sum(s, sh);
