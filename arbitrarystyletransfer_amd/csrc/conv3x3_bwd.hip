@@ -19,6 +19,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include "../../include/ast_hip.h"
+#include "x3.h"
 #include "det.h"
 
 namespace {
@@ -815,13 +816,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3_kernel(WgArgs a) {
       if (e < C::XI) {                                                                                    \
         const int p = e % NPIX, g = (HALF) * 4 + e / NPIX;                                                \
         bf16x8_t pv[3];                                                                                   \
-        _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                   \
-          bf16_t t0_, t1_, t2_;                                                                           \
-          wg_split3(xv[k][j], t0_, t1_, t2_);                                                             \
-          pv[0][j] = t0_;                                                                                 \
-          pv[1][j] = t1_;                                                                                 \
-          pv[2][j] = t2_;                                                                                 \
-        }                                                                                                 \
+        ast_x3::split8(xv[k], pv[0], pv[1], pv[2]);  /* = wg_split3 per value, paired conversions */    \
         const int off = (g >> 2) * C::XHALF + p * C::XROW + (g & 3) * 16;                                 \
         _Pragma("unroll") for (int pl = 0; pl < 3; ++pl)                                                  \
           *reinterpret_cast<u32x4_t*>(wg3_smem + pl * C::XPLANE + off) = __builtin_bit_cast(u32x4_t, pv[pl]); \
@@ -845,14 +840,8 @@ __global__ __launch_bounds__(256, 2) void wgrad3_kernel(WgArgs a) {
       const int e = tid + 256 * k, co = e >> 3, o = e & 7;
       bf16x8_t pv[3];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        bacc[k] += dv[k][j];
-        bf16_t t0_, t1_, t2_;
-        wg_split3(dv[k][j], t0_, t1_, t2_);
-        pv[0][j] = t0_;
-        pv[1][j] = t1_;
-        pv[2][j] = t2_;
-      }
+      for (int j = 0; j < 8; ++j) bacc[k] += dv[k][j];
+      ast_x3::split8(dv[k], pv[0], pv[1], pv[2]);
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
         *reinterpret_cast<u32x4_t*>(wg3_smem + C::DOFF + pl * C::DPLANE + co * C::DP + 16 * o) =

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/ast_hip.h"
+#include "x3.h"
 
 namespace {
 
@@ -531,7 +532,9 @@ struct X3Cfg {
   static constexpr int B_T = (B_UNITS + NT - 1) / NT;
   static constexpr int NS = UP == 1 ? RM + 2 : RM / 2 + 2;  // source rows a wave's RM output rows read
   static constexpr int LDS_TILES = (A_UNITS + B_UNITS) * 16;
-  static constexpr int LDS_EPI = X3_STAGED_EPI ? WM * 32 * RM * 36 * 4 : 0;  // staged epilogue regions
+  // staged epilogue regions: the M16 and persistent kernels always stage through LDS, whatever
+  // X3_STAGED_EPI (which only selects the 32x32 kernel's direct-store A/B form) says
+  static constexpr int LDS_EPI = WM * 32 * RM * 36 * 4;
   static constexpr int LDS_BYTES = LDS_TILES > LDS_EPI ? LDS_TILES : LDS_EPI;
 };
 
@@ -628,6 +631,29 @@ __device__ __forceinline__ void store_tiles_staged(const ConvArgs& a, const f32x
   }
 }
 
+// Diagnostic build only (X3_STAMP=1, scripts/build_variants.sh; never the product library): every
+// wave of the first X3_STAMP_WGS workgroups records the shader-clock counter at its phase boundaries
+// (entry, prologue done, and per K chunk: loads issued / MFMAs done / first barrier / store + second
+// barrier; epilogue start / end) in three VGPRs (lane k holds stamp k), stored once at the end to
+// x3_stamp_buf, which no other code reads; scripts/x3_stamps.py reads it back.
+#ifndef X3_STAMP
+#define X3_STAMP 0
+#endif
+#if X3_STAMP
+constexpr int kX3StampWgs = 2048, kX3StampRec = 200;
+__device__ unsigned x3_stamp_buf[kX3StampWgs * 16 * kX3StampRec];
+#define X3_ST(IDX)                                                                  \
+  {                                                                                 \
+    const unsigned t_ = (unsigned)__builtin_readcyclecounter();                     \
+    const int i_ = (IDX);                                                           \
+    st0 = lane == i_ ? t_ : st0;                                                    \
+    st1 = lane == i_ - 64 ? t_ : st1;                                               \
+    st2 = lane == i_ - 128 ? t_ : st2;                                              \
+  }
+#else
+#define X3_ST(IDX)
+#endif
+
 // M16: the same kernel on v_mfma_f32_16x16x32_bf16 (16 pixels x 16 output channels x K 32). The six
 // split products fold into three K-32 MFMAs -- K = (16 channels of one term | 16 of another):
 //   [x_hi | x_mid] . [w_hi ; w_hi]  = x_hi w_hi  + x_mid w_hi
@@ -649,6 +675,10 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   u32x4* Bs = x3_smem + C::A_UNITS;
 
   const int tid = threadIdx.x, wm = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+#if X3_STAMP
+  unsigned st0 = 0, st1 = 0, st2 = 0;
+  X3_ST(0);
+#endif
   int t, grp;
   if (!decode_block(blockIdx.x, a.tiles_x * a.tiles_y * a.N, (a.Cout + BN - 1) / BN, t, grp)) return;
   const int tx = t % a.tiles_x;
@@ -697,23 +727,30 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   float ra[A_T][8];
   u32x4 rb[B_T];
   // channel ci0 + 8h + j of item i; a partial last chunk clamps the channel (values masked at store)
-#define X3_LOAD(KC)                                                                                     \
+#define X3_LOAD_A(KC, I0, I1)                                                                           \
   {                                                                                                     \
     const int ci0 = (KC) * kX3K;                                                                        \
     if (ci0 + kX3K <= a.Cin) {                                                                          \
       const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(                              \
           const_cast<float*>(xin + (int64_t)ci0 * plane_in), 0, kX3K * plane_b, 0x00020000);           \
       _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                     \
-        _Pragma("unroll") for (int i = 0; i < A_T; ++i)                                                 \
+        _Pragma("unroll") for (int i = (I0); i < (I1); ++i)                                             \
           ra[i][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)g_off[i], j * plane_b, 0)); \
     } else {                                                                                            \
-      _Pragma("unroll") for (int i = 0; i < A_T; ++i)                                                   \
+      _Pragma("unroll") for (int i = (I0); i < (I1); ++i)                                               \
         _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                   \
           ra[i][j] = xin[(int64_t)min(ci0 + 8 * g_h[i] + j, a.Cin - 1) * plane_in + g_pix[i]];          \
     }                                                                                                   \
-    _Pragma("unroll") for (int i = 0; i < B_T; ++i)                                                     \
-      rb[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, b_src[i], (int)((KC) * chunk_units * 16), 0)); \
   }
+#define X3_LOAD_B(KC)                                                                                   \
+  _Pragma("unroll") for (int i = 0; i < B_T; ++i)                                                       \
+    rb[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, b_src[i], (int)((KC) * chunk_units * 16), 0));
+#define X3_LOAD(KC)         \
+  {                         \
+    X3_LOAD_A(KC, 0, A_T);  \
+    X3_LOAD_B(KC);          \
+  }
+  // split into the three term planes (ast_x3::split8: paired conversions, bit-identical to split3)
 #define X3_STORE(KC)                                                                                    \
   {                                                                                                     \
     _Pragma("unroll") for (int i = 0; i < A_T; ++i) {                                                   \
@@ -723,13 +760,7 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
           _Pragma("unroll") for (int j = 0; j < 8; ++j) ra[i][j] = (g_ok[i] && j < cn) ? ra[i][j] : 0.f; \
         }                                                                                               \
         bf16x8 pv[3];                                                                                   \
-        _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                 \
-          bf16 t0, t1, t2;                                                                              \
-          split3(ra[i][j], t0, t1, t2);                                                                 \
-          pv[0][j] = t0;                                                                                \
-          pv[1][j] = t1;                                                                                \
-          pv[2][j] = t2;                                                                                \
-        }                                                                                               \
+        ast_x3::split8(ra[i], pv[0], pv[1], pv[2]);                                                     \
         _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                   \
           As[p * A_PLANE + g_lds[i]] = __builtin_bit_cast(u32x4, pv[p]);                                \
       }                                                                                                 \
@@ -775,8 +806,12 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   X3_LOAD(0);
   X3_STORE(0);
   __syncthreads();
+  X3_ST(1);
+  static_assert(A_T < 9, "one gather item per tap of the MFMA phase");
   for (int kc = 0; kc < nch; ++kc) {
-    if (kc + 1 < nch) X3_LOAD(kc + 1);
+    if (!M16 && kc + 1 < nch) X3_LOAD(kc + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    X3_ST(2 + 4 * kc);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (M16) {
 #pragma unroll
@@ -784,6 +819,15 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
           const int tap = ky * 3 + kx;
+          // the next chunk's global loads, spread over the first taps (one gather item per tap, then
+          // the weight slab): issued all at once they queued behind the CU's memory pipeline for
+          // ~3k cycles per chunk with no MFMA issued (scripts/x3_stamps.py, profiles/r05_x3_stamps.txt)
+          if (kx * 3 + ky <= A_T && kc + 1 < nch) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (kx * 3 + ky < A_T) X3_LOAD_A(kc + 1, kx * 3 + ky, kx * 3 + ky + 1)
+            else X3_LOAD_B(kc + 1)
+            __builtin_amdgcn_sched_barrier(0);
+          }
           bf16x8 g1[Q], g2[Q], g3[Q];
 #pragma unroll
           for (int q = 0; q < Q; ++q) {
@@ -858,18 +902,24 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
       }
     }
     __builtin_amdgcn_sched_barrier(0);
+    X3_ST(3 + 4 * kc);
     if (kc + 1 < nch) {
       __syncthreads();  // every wave is done reading this chunk
+      X3_ST(4 + 4 * kc);
       X3_STORE(kc + 1);
       __syncthreads();
+      X3_ST(5 + 4 * kc);
     }
   }
 #undef X3_LOAD
+#undef X3_LOAD_A
+#undef X3_LOAD_B
 #undef X3_STORE
   if constexpr (M16) {
     // staged epilogue, 32 channels (two 16-tiles) per pass: lane (l16, g16) holds pixels 16 pt + 4 g16
     // + r of channel 16 q + l16 -> one float4 per (row, pixel tile) into the region
     __syncthreads();  // every wave is done reading the last chunk's tiles
+    X3_ST(2 + 4 * nch);
     float* region = reinterpret_cast<float*>(x3_smem) + wm * 32 * RM * 36;
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
@@ -894,6 +944,23 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
         __builtin_amdgcn_wave_barrier();
       }
     }
+#if X3_STAMP
+    __builtin_amdgcn_s_waitcnt(0);  // the epilogue's stores have left (vmcnt 0)
+    X3_ST(3 + 4 * nch);
+    if (blockIdx.x < kX3StampWgs) {
+      unsigned* rec = x3_stamp_buf + ((size_t)blockIdx.x * 16 + wm) * kX3StampRec;
+      rec[lane] = st0;
+      rec[64 + lane] = st1;
+      rec[128 + lane] = st2;
+      if (lane == 0) {
+        rec[192] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_REG_HW_ID: wave, SIMD, CU, SE
+        rec[193] = __builtin_amdgcn_s_getreg(20 | (3 << 11));   // HW_REG_XCC_ID
+        rec[194] = blockIdx.x;
+        rec[195] = nch;
+        rec[196] = 0x57a3u;
+      }
+    }
+#endif
   } else {
 #if X3_STAGED_EPI
     __syncthreads();  // every wave is done reading the last chunk's tiles
@@ -1593,11 +1660,13 @@ int launch_x3p_one(const ConvArgs& a0, hipStream_t s) {
   const int64_t ntiles = (int64_t)a.tiles_x * a.tiles_y * a.N;
   const int64_t nblk = (ntiles + 7) / 8 * 8 * cdiv(a.Cout, C::BN);
   if (nblk >= 0x7fffffff) return AST_E_SHAPE;
-  static int cus = 0;
+  static int cus_of[64] = {};  // CU count per device (looked up on a device's first call)
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int cus = dev >= 0 && dev < 64 ? cus_of[dev] : 0;
   if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (dev >= 0 && dev < 64) cus_of[dev] = cus;
   }
   const int64_t slots = (int64_t)(cus + 7) / 8 * 8 * OCC;
   const unsigned grid = (unsigned)(nblk < slots ? nblk : slots);
@@ -1737,6 +1806,19 @@ int ast_conv3x3_pack_weights_f32(const float* w, float* w_packed, int cout, int 
 }
 
 int ast_conv3x3_num_configs(void) { return kNumConfigs; }
+
+#if X3_STAMP
+// diagnostic build only: copy / clear the stamp records of conv3x3_x3_kernel<M16>
+int ast_dbg_x3_stamps(void* host, size_t bytes, int clear) {
+  const size_t n = std::min(bytes, sizeof(x3_stamp_buf));
+  if (clear) {
+    void* d = nullptr;
+    const hipError_t e = hipGetSymbolAddress(&d, HIP_SYMBOL(x3_stamp_buf));
+    return e ? (int)e : (int)hipMemset(d, 0, sizeof(x3_stamp_buf));
+  }
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(x3_stamp_buf), n, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 int ast_conv3x3_fwd_f32_cfg(int cfg, const float* x, const float* x2, int n2, const float* w_packed,
                             const float* bias, float* y_pre, float* y_act, float* y_pool, const float* in_mean,

@@ -378,8 +378,9 @@ class FlatFolderDatasetAE(FlatFolderDataset):
 # Parallel host decoding (the reference's DataLoader(num_workers=4 | 8), train.py:66-75,
 # train_autoencoder.py:188-195): worker processes open and decode images (PIL, CPU only); the
 # trainer process uploads them and runs ToTensor and every augmentation as HIP kernels, so the GPU is
-# used by one process only. Workers are forked: build the iterator before the process touches the
-# GPU (the helpers below start their workers at once), as the reference builds its loaders first.
+# used by one process only. Workers are forked when the iterator is built before the process touches
+# the GPU (the helpers below start their workers at once), as the reference builds its loaders first;
+# spawned otherwise.
 # ------------------------------------------------------------------------------------------------
 
 class HostDecoded(data.Dataset):
@@ -416,8 +417,12 @@ def device_batches(decoded_iter, transform, pairs=True):
 
 
 def _decoded_loader(dataset, batch_size, num_workers):
+    # forked workers (the default start) only while this process has not initialised the GPU: a fork
+    # of a HIP-initialised process is not safe, so a caller that touched the GPU first gets spawned
+    # workers (they import the package and decode with PIL only)
+    ctx = "spawn" if num_workers > 0 and torch.cuda.is_initialized() else None
     loader = data.DataLoader(HostDecoded(dataset), batch_size=batch_size, sampler=InfiniteSamplerWrapper(dataset),
-                             num_workers=num_workers, collate_fn=_collate_list,
+                             num_workers=num_workers, collate_fn=_collate_list, multiprocessing_context=ctx,
                              persistent_workers=num_workers > 0, prefetch_factor=2 if num_workers > 0 else None)
     return iter(loader)   # starts the workers now (before the caller touches the GPU)
 

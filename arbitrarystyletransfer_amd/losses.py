@@ -20,6 +20,38 @@ def _grad(x):
     return torch.is_grad_enabled() and x.requires_grad
 
 
+class _SymmetricLoss(torch.autograd.Function):
+    """A loss symmetric in its two arguments (L(x, y) = L(y, x): Huber of differences of the two
+    sides' statistics, the EMD of their histograms) differentiated in BOTH, as the reference's own
+    losses are (losses.py:84-87, 124-139 differentiate the target too). The value is fn(x, y); the
+    backward recomputes fn(x, y) for x's gradient and fn(y, x) for y's, through the ops' own HIP
+    backward kernels. Only a grad-requiring target takes this path; every reference caller detaches
+    it (train.py:225-277), and those calls keep the one-sided fused op."""
+
+    @staticmethod
+    def forward(ctx, x, y, fn):
+        ctx.fn = fn
+        ctx.save_for_backward(x, y)
+        return fn(x, y)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        grads = [None, None]
+        with torch.enable_grad():
+            for i, (a, b) in enumerate(((x, y), (y, x))):
+                if ctx.needs_input_grad[i]:
+                    ar = a.detach().requires_grad_(True)
+                    grads[i], = torch.autograd.grad(ctx.fn(ar, b.detach()), ar, g)
+        return grads[0], grads[1], None
+
+
+def _two_sided(fn, x, y):
+    if torch.is_grad_enabled() and y.requires_grad:
+        return _SymmetricLoss.apply(x, y, fn)
+    return fn(x, y.detach())
+
+
 def _pair(x, y, what):
     x, y = _dev(x, "input"), _dev(y, "target")
     if x.shape != y.shape:
@@ -43,9 +75,12 @@ def compute_content_loss(inp, tgt):
 
 
 def compute_style_loss(t_cs_map, style_map):
-    """losses.py:128-139: 1.25*huber(mean) + 1.25*huber(std) + 10*huber(gram). The target is
-    treated as a constant (train.py:233 always passes style_map[i].detach())."""
-    return style_loss_weighted(t_cs_map, style_map, 1.0)
+    """losses.py:128-139: 1.25*huber(mean) + 1.25*huber(std) + 10*huber(gram), differentiable in
+    both arguments as the reference (train.py:233 passes style_map[i].detach(): then only t_cs_map)."""
+    x, y = _dev(t_cs_map, "x"), _dev(style_map, "y")
+    if x.shape[:2] != y.shape[:2] or x.shape[2:] != y.shape[2:]:
+        raise Fn.HipOpError(f"style loss: shape mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
+    return _two_sided(lambda a, b: _ops.style_loss(a, b, 1.0, _grad(a))[0], x, y)
 
 
 def tv_loss(img):
@@ -111,12 +146,13 @@ earth_movers = EarthMoversDistanceLoss()   # losses.py:80
 
 
 def compute_hist_loss(t_cs, style_map, weight: float = 1.0):
-    """losses.py:84-87: earth_movers(hist(t_cs), hist(style_map)).mean(), differentiable in t_cs
-    (style_map is data, train.py:261). `weight` fuses the caller's scale (train.py: 1e-5)."""
-    x, y = _dev(t_cs, "t_cs"), _dev(style_map.detach(), "style_map")
+    """losses.py:84-87: earth_movers(hist(t_cs), hist(style_map)).mean(), differentiable in both
+    arguments as the reference (train.py:261 passes data as style_map). `weight` fuses the caller's
+    scale (train.py: 1e-5)."""
+    x, y = _dev(t_cs, "t_cs"), _dev(style_map, "style_map")
     if x.shape[0] != y.shape[0]:
         raise Fn.HipOpError(f"hist loss: batch mismatch {tuple(x.shape)} vs {tuple(y.shape)}")
-    return _ops.hist_loss(x, y, float(weight))[0]
+    return _two_sided(lambda a, b: _ops.hist_loss(a, b, float(weight))[0], x, y)
 
 
 def out_of_range_loss(img, weight: float = 1e8):

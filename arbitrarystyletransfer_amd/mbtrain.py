@@ -172,9 +172,11 @@ class deferred_bn_counters:
 
     def __exit__(self, *exc):
         global _BN_PENDING
-        self.pool.__exit__(*exc)
-        pend, _BN_PENDING = _BN_PENDING, self.prev
-        if pend:
+        try:
+            self.pool.__exit__(*exc)
+        finally:
+            pend, _BN_PENDING = _BN_PENDING, self.prev
+        if pend and exc[0] is None:   # a step that raised did not complete its forward: no count
             ts = [t for t, _ in pend.values()]
             torch._foreach_add_(ts, [k for _, k in pend.values()])
 

@@ -325,10 +325,12 @@ class ASTTrainer:
         # and SyncBatchNorm's all-gather at world size > 1 has not been verified.
         if graph is None:
             graph = getattr(self.args, "graph", self.world == 1)
-        if graph and self.world > 1 and dist.get_backend() != "nccl":
-            raise ValueError("ASTTrainer(graph=True) needs the nccl (RCCL) backend under data parallelism: "
-                             "gloo collectives stage through the host and cannot be captured")
-        self.graph = graph and grad_hook is None
+        graph = graph and grad_hook is None   # a grad_hook needs the eager step
+        if graph and self.world > 1:
+            raise ValueError("ASTTrainer(graph=True) runs in one process only: gloo collectives stage through "
+                             "the host and cannot be captured, and a captured RCCL all-reduce / SyncBatchNorm "
+                             "all-gather at world size > 1 has not been checked against the eager step")
+        self.graph = graph
         self._step_graph = None
         if self.graph:
             if self.grad_arena is None:   # persistent gradient storage for the captured optimizer tables

@@ -158,3 +158,12 @@ def test_no_packed_fp32_valu_in_kernels(tmp_path):
         assert "s_endpgm" in dis
         bad = [ln.strip() for ln in dis.splitlines() if re.search(r"\bv_pk_(fma|mul|add)_f32\b", ln)]
         assert not bad, (k, bad[:4])
+        # every packed / dual-lane / dot-product VALU opcode still present, decided one by one
+        # (VERDICT r4 next #6): only the two below may appear --
+        #   v_cvt_pk_bf16_f32  fp32 -> bf16 conversion of two operands into ONE dword per lane (the
+        #                      split-bf16 and bf16 kernels' rounding; a plain single-result VALU op)
+        #   v_pk_mov_b32       a 64-bit register move (no arithmetic), emitted for register copies in
+        #                      the MobileNet v2 expand+depthwise and dense 3x3 kernels
+        # any v_pk_* arithmetic (f32/f16/bf16/int), v_dot2*/v_dot4*, v_fma_mix*, v_permlane* fails here
+        found = set(re.findall(r"^\s*(v_(?:pk_\w+|dot\d\w*|fma_mix\w*|mad_mix\w*|permlane\w*|cvt_pk\w*))\b", dis, re.M))
+        assert found <= {"v_cvt_pk_bf16_f32", "v_pk_mov_b32"}, (k, sorted(found))

@@ -35,7 +35,8 @@ def rel_inf(a, b):
 
 
 SMALL_ATT = [((2, 16, 6, 10), (2, 16, 7, 5)), ((1, 128, 16, 12), (1, 128, 9, 20)), ((2, 128, 8, 8), (2, 128, 8, 8)),
-             ((1, 96, 9, 11), (1, 96, 5, 13))]
+             ((1, 96, 9, 11), (1, 96, 5, 13)),
+             ((2, 48, 7, 9), (2, 48, 11, 6)), ((1, 64, 13, 10), (1, 64, 6, 15))]   # CT = 3, 4 builds, ragged
 
 
 @pytest.mark.parametrize("shape,mode", [(s, m) for s in SMALL_ATT for m in ("auto", "flash")] +

@@ -189,6 +189,37 @@ def test_style_loss_vs_oracle(shape, hip_device):
     assert rel_inf(xd.grad, xr.grad) <= TOL
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 24, 20), (1, 3, 33, 17)])
+def test_losses_differentiate_the_target(shape, hip_device):
+    """The drop-in losses take a grad-requiring target as the reference does (losses.py:84-87,
+    124-139 differentiate both arguments): value and BOTH gradients against CPU autograd of the
+    oracle. The reference callers detach the target (train.py:225-277); this is the drop-in case."""
+    x = rnd(91, shape, 1.0, 0.5)
+    y = rnd(92, shape, 1.2, 0.3)
+    img = (shape[1] == 3)
+    cases = [("style", L.compute_style_loss, R.compute_style_loss, 2e-5),
+             ("content", L.compute_content_loss, R.compute_content_loss, 2e-5)]
+    if img:   # the soft histogram is defined on [0, 1] images (train.py:261)
+        x, y = x.clamp(0, 1), y.clamp(0, 1)
+        cases.append(("hist", L.compute_hist_loss, R.compute_hist_loss, 1e-4))
+    for name, fn, ref_fn, tol in cases:
+        xr, yr = x.double().requires_grad_(), y.double().requires_grad_()
+        ref = ref_fn(xr, yr)
+        ref.backward()
+        xd, yd = x.to(hip_device).requires_grad_(), y.to(hip_device).requires_grad_()
+        got = fn(xd, yd)
+        got.backward()
+        np.testing.assert_allclose(got.item(), ref.item(), rtol=2e-5, err_msg=name)
+        assert rel_inf(xd.grad, xr.grad) <= tol, name
+        assert rel_inf(yd.grad, yr.grad) <= tol, name
+        # a detached target: the one-sided fused op, the same value and x gradient
+        xd2 = x.to(hip_device).requires_grad_()
+        one = fn(xd2, y.to(hip_device))
+        one.backward()
+        np.testing.assert_allclose(one.item(), got.item(), rtol=1e-6, err_msg=name)
+        assert torch.equal(xd2.grad, xd.grad), name
+
+
 @pytest.mark.parametrize("shape,offset", [((16, 3, 512, 512), 0), ((1, 2, 300, 300), 0), ((2, 3, 37, 41), 0),
                                           ((4, 8, 96, 96), 1), ((3, 64, 64, 64), 0)])
 def test_plane_stats_losses_vs_oracle(shape, offset, hip_device):
@@ -526,8 +557,9 @@ def test_full_losses_step_with_grad_arena(hip_device):
         assert np.mean(diff > 1e-6) <= 1e-3 and diff.max() <= 4e-4
 
 
-@pytest.mark.parametrize("global_batch,full,nproc", [(3, False, 2), (2, True, 2), (61, False, 8)])
-def test_adain_dp_ranks_match_single_process(global_batch, full, nproc, tmp_path, hip_device):
+@pytest.mark.parametrize("global_batch,full,nproc,size", [(3, False, 2, 64), (2, True, 2, 64), (61, False, 8, 64),
+                                                       (16, False, 8, 512)])
+def test_adain_dp_ranks_match_single_process(global_batch, full, nproc, size, tmp_path, hip_device):
     """BASELINE.json config 4 on the HIP path: two ranks
     (torch.distributed.run, gloo on the one GPU) each run AdaINTrainer on their shard of the global
     batch (3 images: uneven 2 + 1 shards; 2 images with the full train.py loss), the decoder
@@ -535,7 +567,10 @@ def test_adain_dp_ranks_match_single_process(global_batch, full, nproc, tmp_path
     the updated weights must equal one process stepping the whole batch (train.py:287-300).
     nproc 8: config 4's world size, 8 ranks on the one GPU, global batch 61 in
     uneven shards 8,8,8,8,8,7,7,7 (config 4 itself is 64 = 8 x 8 at 512^2, one rank per GPU over
-    RCCL: the driver's multi-GPU run)."""
+    RCCL: the driver's multi-GPU run). nproc 8 at size 512: config 4's
+    per-rank workload at its full image size -- 8 ranks x 2 images of 512^2 (the arena and the
+    loss network's per-rank maps at their real sizes; 8 x 8 would not fit eight processes' step
+    memory on one GPU) against one process stepping all 16."""
     import os
     import socket
     import subprocess
@@ -544,12 +579,11 @@ def test_adain_dp_ranks_match_single_process(global_batch, full, nproc, tmp_path
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    size = 64
     out = str(tmp_path / "dp.npz")
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "adain_dp_worker.py")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                         "--master-addr=127.0.0.1", f"--master-port={port}", worker, out, str(global_batch), str(size)]
-                       + (["full"] if full else []), capture_output=True, text=True, timeout=240)
+                       + (["full"] if full else []), capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     got = np.load(out)
     grads, params, norm = _single_process_step(hip_device, global_batch, size, full)
