@@ -725,7 +725,8 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
     b_dst[i] = u;
   }
   float ra[A_T][8];
-  u32x4 rb[B_T];
+  u32x4 rb[M16 ? 1 : B_T];
+  bf16x8 pv[M16 ? A_T : 1][3];
   // channel ci0 + 8h + j of item i; a partial last chunk clamps the channel (values masked at store)
 #define X3_LOAD_A(KC, I0, I1)                                                                           \
   {                                                                                                     \
@@ -743,8 +744,38 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
     }                                                                                                   \
   }
 #define X3_LOAD_B(KC)                                                                                   \
-  _Pragma("unroll") for (int i = 0; i < B_T; ++i)                                                       \
+  _Pragma("unroll") for (int i = 0; i < (M16 ? 0 : B_T); ++i)                                           \
     rb[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, b_src[i], (int)((KC) * chunk_units * 16), 0));
+  // M16: the weight slab goes global -> LDS by LDS-DMA (global_load_lds_dwordx4, one lane-linear
+  // 1-KiB piece of the slab per wave-instruction, no VGPRs and no ds_write), issued right after the
+  // barrier that frees Bs; the barrier after the A tile's writes waits for it (vmcnt(0))
+  constexpr int B_PIECES = C::B_UNITS / 64, BP_T = (B_PIECES + WM - 1) / WM;
+  static_assert(C::B_UNITS % 64 == 0, "whole 1-KiB pieces");
+#define X3_DMA_B(KC)                                                                                    \
+  _Pragma("unroll") for (int i = 0; i < BP_T; ++i) {                                                    \
+    const int piece = wm + i * WM;                                                                      \
+    if (piece < B_PIECES) {                                                                             \
+      const int u = piece * 64 + lane, row = u / BN, j = u - row * BN;                                  \
+      const u32x4* src = wsplit + (int64_t)(KC) * chunk_units + (int64_t)row * a.cout_pad + n0 + j;     \
+      __builtin_amdgcn_global_load_lds((const void*)src,                                                \
+                                       (__attribute__((address_space(3))) void*)(Bs + piece * 64), 16, 0, 0); \
+    }                                                                                                   \
+  }
+  // M16: the gathered x split into its term planes in registers (before the barrier, in the slack of
+  // a wave that finished its MFMAs early), written after it
+#define X3_SPLIT_A(KC)                                                                                  \
+  _Pragma("unroll") for (int i = 0; i < A_T; ++i) {                                                     \
+    if ((KC) * kX3K + kX3K > a.Cin) { /* partial last chunk: padding and channels past Cin */            \
+      const int cn = a.Cin - (KC) * kX3K - 8 * g_h[i];                                                  \
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) ra[i][j] = (g_ok[i] && j < cn) ? ra[i][j] : 0.f;     \
+    }                                                                                                   \
+    ast_x3::split8(ra[i], pv[i][0], pv[i][1], pv[i][2]);                                                \
+  }
+#define X3_WRITE_A                                                                                      \
+  _Pragma("unroll") for (int i = 0; i < A_T; ++i)                                                       \
+    if (tid + i * NT < A_ITEMS)                                                                         \
+      _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                     \
+        As[p * A_PLANE + g_lds[i]] = __builtin_bit_cast(u32x4, pv[i][p]);
 #define X3_LOAD(KC)         \
   {                         \
     X3_LOAD_A(KC, 0, A_T);  \
@@ -803,8 +834,15 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   const int apl1 = (g16 < 2 ? 0 : 1) * A_PLANE, apl2 = (g16 < 2 ? 0 : 2) * A_PLANE;  // [hi|mid], [hi|lo]
   const int bpl1 = 0, bpl2 = g16 < 2 ? 1 : 0, bpl3 = g16 < 2 ? 2 : 1;  // [hi;hi], [mid;hi], [lo;mid]
 
-  X3_LOAD(0);
-  X3_STORE(0);
+  if constexpr (M16) {
+    X3_DMA_B(0);
+    X3_LOAD_A(0, 0, A_T);
+    X3_SPLIT_A(0);
+    X3_WRITE_A;
+  } else {
+    X3_LOAD(0);
+    X3_STORE(0);
+  }
   __syncthreads();
   X3_ST(1);
   static_assert(A_T < 9, "one gather item per tap of the MFMA phase");
@@ -822,10 +860,9 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
           // the next chunk's global loads, spread over the first taps (one gather item per tap, then
           // the weight slab): issued all at once they queued behind the CU's memory pipeline for
           // ~3k cycles per chunk with no MFMA issued (scripts/x3_stamps.py, profiles/r05_x3_stamps.txt)
-          if (kx * 3 + ky <= A_T && kc + 1 < nch) {
+          if (kx * 3 + ky < A_T && kc + 1 < nch) {
             __builtin_amdgcn_sched_barrier(0);
-            if (kx * 3 + ky < A_T) X3_LOAD_A(kc + 1, kx * 3 + ky, kx * 3 + ky + 1)
-            else X3_LOAD_B(kc + 1)
+            X3_LOAD_A(kc + 1, kx * 3 + ky, kx * 3 + ky + 1)
             __builtin_amdgcn_sched_barrier(0);
           }
           bf16x8 g1[Q], g2[Q], g3[Q];
@@ -904,9 +941,17 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     X3_ST(3 + 4 * kc);
     if (kc + 1 < nch) {
-      __syncthreads();  // every wave is done reading this chunk
-      X3_ST(4 + 4 * kc);
-      X3_STORE(kc + 1);
+      if constexpr (M16) {
+        X3_SPLIT_A(kc + 1);
+        __syncthreads();  // every wave is done reading this chunk
+        X3_ST(4 + 4 * kc);
+        X3_DMA_B(kc + 1);
+        X3_WRITE_A;
+      } else {
+        __syncthreads();  // every wave is done reading this chunk
+        X3_ST(4 + 4 * kc);
+        X3_STORE(kc + 1);
+      }
       __syncthreads();
       X3_ST(5 + 4 * kc);
     }
@@ -915,6 +960,9 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
 #undef X3_LOAD_A
 #undef X3_LOAD_B
 #undef X3_STORE
+#undef X3_DMA_B
+#undef X3_SPLIT_A
+#undef X3_WRITE_A
   if constexpr (M16) {
     // staged epilogue, 32 channels (two 16-tiles) per pass: lane (l16, g16) holds pixels 16 pt + 4 g16
     // + r of channel 16 q + l16 -> one float4 per (row, pixel tile) into the region
