@@ -536,6 +536,10 @@ struct X3Cfg {
   // X3_STAGED_EPI (which only selects the 32x32 kernel's direct-store A/B form) says
   static constexpr int LDS_EPI = WM * 32 * RM * 36 * 4;
   static constexpr int LDS_BYTES = LDS_TILES > LDS_EPI ? LDS_TILES : LDS_EPI;
+  // M16 kernel: A tile, the weight slab's lo plane, and its hi + mid planes twice (the next chunk's
+  // arrive by LDS-DMA during the current chunk's MFMAs)
+  static constexpr int LDS_TILES_M16 = (A_UNITS + 18 * BN + 2 * 36 * BN) * 16;
+  static constexpr int LDS_BYTES_M16 = LDS_TILES_M16 > LDS_EPI ? LDS_TILES_M16 : LDS_EPI;
 };
 
 // source row (relative to the wave's first) of output row i at tap row ky
@@ -673,6 +677,9 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) u32x4 x3_smem[];
   u32x4* As = x3_smem;
   u32x4* Bs = x3_smem + C::A_UNITS;
+  // M16: [lo plane][hi + mid planes, buffer 0][hi + mid planes, buffer 1] after the A tile
+  u32x4* Blo = x3_smem + C::A_UNITS;
+  u32x4* Bhm0 = Blo + 18 * BN;
 
   const int tid = threadIdx.x, wm = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
 #if X3_STAMP
@@ -749,18 +756,21 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   // M16: the weight slab goes global -> LDS by LDS-DMA (global_load_lds_dwordx4, one lane-linear
   // 1-KiB piece of the slab per wave-instruction, no VGPRs and no ds_write), issued right after the
   // barrier that frees Bs; the barrier after the A tile's writes waits for it (vmcnt(0))
-  constexpr int B_PIECES = C::B_UNITS / 64, BP_T = (B_PIECES + WM - 1) / WM;
-  static_assert(C::B_UNITS % 64 == 0, "whole 1-KiB pieces");
-#define X3_DMA_B(KC)                                                                                    \
-  _Pragma("unroll") for (int i = 0; i < BP_T; ++i) {                                                    \
+  // slab rows (plane, tap, half): hi + mid planes = rows 0-35, lo plane = rows 36-53
+  static_assert((36 * BN) % 64 == 0 && (18 * BN) % 64 == 0, "whole 1-KiB pieces");
+  constexpr int HM_PIECES = 36 * BN / 64, LO_PIECES = 18 * BN / 64;
+#define X3_DMA_ROWS(KC, ROW0, NPIECES, DST)                                                             \
+  _Pragma("unroll") for (int i = 0; i < ((NPIECES) + WM - 1) / WM; ++i) {                               \
     const int piece = wm + i * WM;                                                                      \
-    if (piece < B_PIECES) {                                                                             \
+    if (piece < (NPIECES)) {                                                                            \
       const int u = piece * 64 + lane, row = u / BN, j = u - row * BN;                                  \
-      const u32x4* src = wsplit + (int64_t)(KC) * chunk_units + (int64_t)row * a.cout_pad + n0 + j;     \
+      const u32x4* src = wsplit + (int64_t)(KC) * chunk_units + (int64_t)((ROW0) + row) * a.cout_pad + n0 + j; \
       __builtin_amdgcn_global_load_lds((const void*)src,                                                \
-                                       (__attribute__((address_space(3))) void*)(Bs + piece * 64), 16, 0, 0); \
+                                       (__attribute__((address_space(3))) void*)((DST) + piece * 64), 16, 0, 0); \
     }                                                                                                   \
   }
+#define X3_DMA_HM(KC) X3_DMA_ROWS(KC, 0, HM_PIECES, Bhm0 + ((KC) & 1) * 36 * BN)
+#define X3_DMA_LO(KC) X3_DMA_ROWS(KC, 36, LO_PIECES, Blo)
   // M16: the gathered x split into its term planes in registers (before the barrier, in the slack of
   // a wave that finished its MFMAs early), written after it
 #define X3_SPLIT_A(KC)                                                                                  \
@@ -832,10 +842,10 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) acol16[pt][kx] = ((x0 + 16 * pt + l16 + kx - 1) >> (UP - 1)) - sx0 + 1;
   const int apl1 = (g16 < 2 ? 0 : 1) * A_PLANE, apl2 = (g16 < 2 ? 0 : 2) * A_PLANE;  // [hi|mid], [hi|lo]
-  const int bpl1 = 0, bpl2 = g16 < 2 ? 1 : 0, bpl3 = g16 < 2 ? 2 : 1;  // [hi;hi], [mid;hi], [lo;mid]
 
   if constexpr (M16) {
-    X3_DMA_B(0);
+    X3_DMA_HM(0);
+    X3_DMA_LO(0);
     X3_LOAD_A(0, 0, A_T);
     X3_SPLIT_A(0);
     X3_WRITE_A;
@@ -852,56 +862,96 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
     X3_ST(2 + 4 * kc);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (M16) {
+      // Software-pipelined MFMA phase (round 5): steps s = (kx, ky, row i), kx outermost; the LDS operands of step s + 1 (its A fragments and, when it opens a
+      // tap, the tap's B fragments) are read while step s's MFMAs run. The stamps showed the wave
+      // that finishes a chunk last, alone on its SIMD, issuing MFMAs at ~70% of the pipe rate: each
+      // step waited on reads issued just before it (profiles/r05_x3_stamps.txt). Same products in
+      // the same order per accumulator as the round-4 loop: bit-identical.
+      constexpr int NSTEP = 9 * RM;
+      bf16x8 gb[2][3][Q];  // B fragments (g1, g2, g3) of a tap, by tap parity
+      bf16x8 fa[2][2][2];  // A fragments (f1, f2) x pixel tile of a step, by step parity
+      // this chunk's B planes: g1 = [hi; hi], g2 = [mid | hi; hi], g3 = [lo; mid] by k-group
+      const u32x4* __restrict__ bhm = Bhm0 + (kc & 1) * 36 * BN;
+      const u32x4* __restrict__ bp1 = bhm;                                         // hi
+      const u32x4* __restrict__ bp2 = bhm + (g16 < 2 ? 18 * BN : 0);               // mid | hi
+      const u32x4* __restrict__ bp3 = g16 < 2 ? Blo : bhm + 18 * BN;               // lo | mid
+#define X3P_READ_B(BUF, T)                                                                              \
+      {                                                                                                 \
+        const int tap_ = ((T) % 3) * 3 + (T) / 3;                                                       \
+        _Pragma("unroll") for (int q = 0; q < Q; ++q) {                                                 \
+          const int col = q * 16 + l16;                                                                 \
+          gb[BUF][0][q] = __builtin_bit_cast(bf16x8, bp1[(tap_ * 2 + hh16) * BN + col]);               \
+          gb[BUF][1][q] = __builtin_bit_cast(bf16x8, bp2[(tap_ * 2 + hh16) * BN + col]);               \
+          gb[BUF][2][q] = __builtin_bit_cast(bf16x8, bp3[(tap_ * 2 + hh16) * BN + col]);               \
+        }                                                                                               \
+      }
+#define X3P_READ_A(BUF, S)                                                                              \
+      {                                                                                                 \
+        const int t_ = (S) / RM, i_ = (S) % RM, kx_ = t_ / 3, ky_ = t_ % 3;                             \
+        const int srow = hh16 * HS + (srow0 + x3_srel<UP>(i_, ky_)) * SC;                               \
+        _Pragma("unroll") for (int pt = 0; pt < 2; ++pt) {                                              \
+          fa[BUF][0][pt] = __builtin_bit_cast(bf16x8, As[apl1 + srow + acol16[pt][kx_]]);               \
+          fa[BUF][1][pt] = __builtin_bit_cast(bf16x8, As[apl2 + srow + acol16[pt][kx_]]);               \
+        }                                                                                               \
+      }
+      X3P_READ_B(0, 0);
+      X3P_READ_A(0, 0);
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          const int tap = ky * 3 + kx;
-          // the next chunk's global loads, spread over the first taps (one gather item per tap, then
-          // the weight slab): issued all at once they queued behind the CU's memory pipeline for
-          // ~3k cycles per chunk with no MFMA issued (scripts/x3_stamps.py, profiles/r05_x3_stamps.txt)
-          if (kx * 3 + ky < A_T && kc + 1 < nch) {
-            __builtin_amdgcn_sched_barrier(0);
-            X3_LOAD_A(kc + 1, kx * 3 + ky, kx * 3 + ky + 1)
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          bf16x8 g1[Q], g2[Q], g3[Q];
-#pragma unroll
-          for (int q = 0; q < Q; ++q) {
-            const int col = q * 16 + l16;
-            g1[q] = __builtin_bit_cast(bf16x8, Bs[((bpl1 * 9 + tap) * 2 + hh16) * BN + col]);
-            g2[q] = __builtin_bit_cast(bf16x8, Bs[((bpl2 * 9 + tap) * 2 + hh16) * BN + col]);
-            g3[q] = __builtin_bit_cast(bf16x8, Bs[((bpl3 * 9 + tap) * 2 + hh16) * BN + col]);
-          }
-#pragma unroll
-          for (int i = 0; i < RM; ++i) {
-            const int srow = hh16 * HS + (srow0 + x3_srel<UP>(i, ky)) * SC;
-            bf16x8 f1[2], f2[2];
-#pragma unroll
-            for (int pt = 0; pt < 2; ++pt) {
-              f1[pt] = __builtin_bit_cast(bf16x8, As[apl1 + srow + acol16[pt][kx]]);
-              f2[pt] = __builtin_bit_cast(bf16x8, As[apl2 + srow + acol16[pt][kx]]);
-            }
-            // the three products of an accumulator in the same order, but product-major: 2Q
-            // independent MFMAs separate each from the next one on the same accumulator
-#pragma unroll
-            for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-              for (int q = 0; q < Q; ++q)
-                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g3[q], acc16[i][pt][q], 0, 0, 0);
-#pragma unroll
-            for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-              for (int q = 0; q < Q; ++q)
-                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[pt], g2[q], acc16[i][pt][q], 0, 0, 0);
-#pragma unroll
-            for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-              for (int q = 0; q < Q; ++q)
-                acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[pt], g1[q], acc16[i][pt][q], 0, 0, 0);
+      for (int st = 0; st < NSTEP; ++st) {
+        const int t = st / RM, i = st % RM, sb = st & 1, tb = t & 1;
+        // the next chunk's global loads, spread over the first taps (one gather item per tap):
+        // issued all at once they queued behind the CU's memory pipeline for ~3k cycles per chunk
+        // with no MFMA issued (scripts/x3_stamps.py, profiles/r05_x3_stamps.txt)
+        if (i == 0 && t < A_T && kc + 1 < nch) {
+          __builtin_amdgcn_sched_barrier(0);
+          X3_LOAD_A(kc + 1, t, t + 1)
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // the next chunk's hi + mid weight planes into the other buffer (LDS-DMA, no VGPRs)
+        if (i == 0 && t == A_T && kc + 1 < nch) {
+          __builtin_amdgcn_sched_barrier(0);
+          X3_DMA_HM(kc + 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        int nrd = 0;
+        if (st + 1 < NSTEP) {
+          X3P_READ_A(sb ^ 1, st + 1);
+          nrd = 4;
+          if ((st + 1) % RM == 0) {
+            X3P_READ_B(tb ^ 1, (st + 1) / RM);
+            nrd += 3 * Q;
           }
         }
+        // the three products of an accumulator in the same order, but product-major: 2Q
+        // independent MFMAs separate each from the next one on the same accumulator
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[sb][0][pt], gb[tb][2][q], acc16[i][pt][q], 0, 0, 0);
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[sb][1][pt], gb[tb][1][q], acc16[i][pt][q], 0, 0, 0);
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            acc16[i][pt][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[sb][0][pt], gb[tb][0][q], acc16[i][pt][q], 0, 0, 0);
+        // one LDS read per MFMA while the next step's reads last, then the rest of the MFMAs
+#pragma unroll
+        for (int r = 0; r < nrd; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        if (nrd == 4) __builtin_amdgcn_sched_group_barrier(0x008, 6 * Q - 4, 0);
+        else if (nrd == 4 + 3 * Q) __builtin_amdgcn_sched_group_barrier(0x008, 3 * Q - 4, 0);
+        else __builtin_amdgcn_sched_group_barrier(0x008, 6 * Q, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
+#undef X3P_READ_A
+#undef X3P_READ_B
     } else {
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
@@ -945,7 +995,7 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
         X3_SPLIT_A(kc + 1);
         __syncthreads();  // every wave is done reading this chunk
         X3_ST(4 + 4 * kc);
-        X3_DMA_B(kc + 1);
+        X3_DMA_LO(kc + 1);
         X3_WRITE_A;
       } else {
         __syncthreads();  // every wave is done reading this chunk
@@ -960,7 +1010,9 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
 #undef X3_LOAD_A
 #undef X3_LOAD_B
 #undef X3_STORE
-#undef X3_DMA_B
+#undef X3_DMA_ROWS
+#undef X3_DMA_HM
+#undef X3_DMA_LO
 #undef X3_SPLIT_A
 #undef X3_WRITE_A
   if constexpr (M16) {
@@ -1688,12 +1740,14 @@ int launch_x3_one(const ConvArgs& a0, hipStream_t s) {
   const int64_t nblk = (ntiles + 7) / 8 * 8 * cdiv(a.Cout, C::BN);
   if (nblk >= 0x7fffffff) return AST_E_SHAPE;
   auto kern = conv3x3_x3_kernel<WM, RM, RN, UP, OCC, M16>;
+  constexpr int lds = M16 ? C::LDS_BYTES_M16 : C::LDS_BYTES;
+  static_assert(lds * OCC <= 160 * 1024, "LDS per CU");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(C::NT), C::LDS_BYTES, s, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(C::NT), lds, s, a);
   return (int)hipGetLastError();
 }
 
