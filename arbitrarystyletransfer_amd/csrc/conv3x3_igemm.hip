@@ -654,8 +654,11 @@ __device__ unsigned x3_stamp_buf[kX3StampWgs * 16 * kX3StampRec];
     st1 = lane == i_ - 64 ? t_ : st1;                                               \
     st2 = lane == i_ - 128 ? t_ : st2;                                              \
   }
+#define X3_ST_STEP(KC, NCH, ST)                                                        \
+  if ((KC) == 5) X3_ST(4 + 4 * (NCH) + (ST))  /* per-step stamps of chunk 5 */
 #else
 #define X3_ST(IDX)
+#define X3_ST_STEP(KC, NCH, ST)
 #endif
 
 // M16: the same kernel on v_mfma_f32_16x16x32_bf16 (16 pixels x 16 output channels x K 32). The six
@@ -899,6 +902,7 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
 #pragma unroll
       for (int st = 0; st < NSTEP; ++st) {
         const int t = st / RM, i = st % RM, sb = st & 1, tb = t & 1;
+        X3_ST_STEP(kc, nch, st);
         // the next chunk's global loads, spread over the first taps (one gather item per tap):
         // issued all at once they queued behind the CU's memory pipeline for ~3k cycles per chunk
         // with no MFMA issued (scripts/x3_stamps.py, profiles/r05_x3_stamps.txt)

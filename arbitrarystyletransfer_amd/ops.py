@@ -91,7 +91,8 @@ def tuned_config(n, cin, h_in, w_in, cout, up, pad_mode, pool) -> int:
     if _TUNING is None:
         import json
         import os
-        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tuning.json")
+        path = os.environ.get("AST_CONV_TUNING") or os.path.join(  # override: A/B of tuning tables
+            os.path.dirname(os.path.abspath(__file__)), "conv_tuning.json")
         try:
             with open(path) as f:
                 _TUNING = json.load(f)
