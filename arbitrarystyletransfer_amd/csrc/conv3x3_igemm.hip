@@ -1514,6 +1514,117 @@ __global__ __launch_bounds__(256, 3) void conv3x3_smallc_kernel(ConvArgs a) {
   }
 }
 
+// Direct (VALU) 3x3 conv for cout <= 4, register-streaming form (round 5; configs 36, 37): no LDS
+// tile and no barrier per input channel. A wave owns 2 output rows x 256 columns (4 per lane); per
+// input channel each lane loads its 4 source rows as one 16-byte piece each, takes the columns left
+// and right of its piece from the neighbouring lanes (the wave's edge lanes and the image borders
+// load theirs), and accumulates 2 rows x 4 pixels x COUT outputs over the 9 taps (weights: one LDS
+// broadcast float4 per tap). The next channel's rows are in flight during the current channel's
+// FMAs. Same tap-major, channel-minor FMA order per output as conv3x3_smallc_kernel: bit-identical.
+// The smallc form stages 4-channel chunks in LDS behind two barriers each and ran at ~2 TB/s of its
+// input (latency-bound, 8x64x512^2 -> 3: 0.27 ms); this one streams.
+template <int COUT>
+__global__ __launch_bounds__(256) void conv3x3_smallc2_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float Wsm[];  // [cin][9 taps][4 co]
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  int t = blockIdx.x;
+  const int bx = t % a.tiles_x;
+  t /= a.tiles_x;
+  const int by = t % a.tiles_y;
+  const int n = t / a.tiles_y;
+  const int H = a.H, W = a.W, Cin = a.Cin;
+  const int x = bx * 256 + 4 * lane, y0 = by * 8 + 2 * wv;
+  for (int e = tid; e < Cin * 36; e += 256) {
+    const int ci = e / 36, rem = e - ci * 36, tap = rem >> 2, co = rem & 3;
+    Wsm[e] = co < COUT ? a.wp[((int64_t)ci * 9 + tap) * a.cout_pad + co] : 0.f;
+  }
+  __syncthreads();
+  const float* __restrict__ xin =
+      n < a.nsplit ? a.x + (int64_t)n * Cin * H * W : a.x2 + (int64_t)(n - a.nsplit) * Cin * H * W;
+  const int64_t plane = (int64_t)H * W;
+  // source rows y0 - 1 .. y0 + 2 (zero pad: -1 = none; reflect: mirrored)
+  int srow[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) srow[r] = src_index<1>(y0 - 1 + r, H, a.reflect);
+  const bool inx = x < W;                                      // W % 4 == 0 (host)
+  const int xl = src_index<1>(x - 1, W, a.reflect), xr = src_index<1>(x + 4, W, a.reflect);
+  const bool own_l = lane == 0 || x == 0, own_r = lane == 63 || x + 4 >= W;  // load the neighbour itself
+  float acc[2][COUT][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int co = 0; co < COUT; ++co)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][co][j] = 0.f;
+  float4 cen[4];
+  float el[4], er[4];
+  auto load = [&](int c, float4 (&cv)[4], float (&l)[4], float (&r)[4]) {
+    const float* xc = xin + (int64_t)c * plane;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = srow[k] >= 0;
+      const float* row = xc + (int64_t)(ok ? srow[k] : 0) * W;
+      cv[k] = (ok && inx) ? *reinterpret_cast<const float4*>(row + x) : make_float4(0.f, 0.f, 0.f, 0.f);
+      l[k] = (ok && own_l && xl >= 0) ? row[xl] : 0.f;
+      r[k] = (ok && own_r && xr >= 0) ? row[xr] : 0.f;
+    }
+  };
+  load(0, cen, el, er);
+  for (int c = 0; c < Cin; ++c) {
+    float4 ncen[4];
+    float nel[4], ner[4];
+    if (c + 1 < Cin) load(c + 1, ncen, nel, ner);
+    float v[4][6];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float left = __shfl_up(cen[k].w, 1, 64), right = __shfl_down(cen[k].x, 1, 64);
+      v[k][0] = own_l ? el[k] : left;
+      v[k][1] = cen[k].x;
+      v[k][2] = cen[k].y;
+      v[k][3] = cen[k].z;
+      v[k][4] = cen[k].w;
+      v[k][5] = own_r ? er[k] : right;
+    }
+    const float4* wc = reinterpret_cast<const float4*>(Wsm + c * 36);
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const float4 w4 = wc[ky * 3 + kx];
+        const float wco[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int co = 0; co < COUT; ++co)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][co][j] = fmaf(v[i + ky][j + kx], wco[co], acc[i][co][j]);
+      }
+    if (c + 1 < Cin) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        cen[k] = ncen[k];
+        el[k] = nel[k];
+        er[k] = ner[k];
+      }
+    }
+  }
+  if (!inx) return;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int yy = y0 + i;
+    if (yy >= H) continue;
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+      if (co >= a.Cout) break;
+      const float bv = a.bias ? a.bias[co] : 0.f;
+      const float4 o = make_float4(acc[i][co][0] + bv, acc[i][co][1] + bv, acc[i][co][2] + bv, acc[i][co][3] + bv);
+      const int64_t off = (((int64_t)n * a.Cout + co) * H + yy) * W + x;
+      if (a.y_pre) *reinterpret_cast<float4*>(a.y_pre + off) = o;
+      if (a.y_act) *reinterpret_cast<float4*>(a.y_act + off) = make_float4(relu_f(o.x), relu_f(o.y), relu_f(o.z), relu_f(o.w));
+    }
+  }
+}
+
 // Direct (VALU) 3x3 conv for cin <= 4 — VGG conv_1 (3->64, models.py:199-216, with the
 // Normalization of models.py:120-131 applied in the gather). As an implicit GEMM its K = 27 runs
 // in 4-channel K-chunks behind 64-channel MFMA tiles and the launch is bound by writing 21x its
@@ -1707,6 +1818,25 @@ int launch_smallc(const ConvArgs& a0, hipStream_t s, int up) {
   return (int)hipGetLastError();
 }
 
+template <int COUT>
+int launch_smallc2(const ConvArgs& a0, hipStream_t s, int up) {
+  ConvArgs a = a0;
+  if (a.Cout > COUT || a.y_pool || up != 1 || (a.W & 3) || a.in_mean || a.Cin > 1024) return AST_E_UNSUPPORTED;
+  a.tiles_x = cdiv(a.W, 256);
+  a.tiles_y = cdiv(a.H, 8);
+  const int64_t nblk = (int64_t)a.tiles_x * a.tiles_y * a.N;
+  if (nblk >= 0x7fffffff) return AST_E_SHAPE;
+  const int lds = a.Cin * 36 * 4;
+  auto kern = conv3x3_smallc2_kernel<COUT>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 1024 * 36 * 4);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(256), lds, s, a);
+  return (int)hipGetLastError();
+}
+
 template <int TH, bool NTS, int OCC = 1>
 int launch_cin4(const ConvArgs& a0, hipStream_t s, int up) {
   ConvArgs a = a0;
@@ -1853,10 +1983,16 @@ const CfgEntry kConfigs[] = {
     {launch_x3p<4, 2, 2>, 64, 8, 2, 0},                 // 33: as 29
     {launch_x3p<4, 2, 1, 2>, 32, 8, 2, 0},              // 34: as 30
     {launch_x3p<8, 2, 1, 1>, 32, 16, 2, 0},             // 35: as 31
+    // register-streaming direct VALU conv for cout <= 4 (no LDS tile, no per-channel barrier)
+    {launch_smallc2<3>, 4, 8, 2, 3},                    // 36: cout <= 3
+    {launch_smallc2<4>, 4, 8, 2, 4},                    // 37: cout <= 4
 };
 constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
 int auto_config(int cin, int cout, int n, int h, int w, int up, bool pool, bool norm) {
+  // cout <= 4: the register-streaming direct conv where it applies (W % 4 == 0, no upsample / pool /
+  // normalisation), else the LDS-staged one (profiles/r05_smallc.txt: 8x64x512^2 -> 3, 0.294 -> 0.226 ms)
+  if (cout <= 4 && up == 1 && !pool && !norm && (w & 3) == 0) return cout <= 3 ? 36 : 37;
   if (cout <= 3) return 10;
   if (cout <= 4) return 11;
   if (cin <= 4 && up == 1 && !pool) return 20;  // direct conv: image-input convs (conv_1)

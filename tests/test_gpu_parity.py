@@ -370,3 +370,37 @@ def test_torch_ops_equal_ctypes_path(hip_device):
     from arbitrarystyletransfer_amd import losses as L
     g1 = o.gram(f)
     assert torch.equal(g1, L.gram_matrix(f))   # split-K partials summed in split order: same bits
+
+
+SMALLC_CASES = [
+    # n, cin, h, w, cout, pad: the cout <= 4 convs (decoder image conv 64 -> 3, the loss network's
+    # conv_1 input gradient 64 -> 3) at tile-ragged sizes
+    (1, 64, 32, 96, 3, "reflect"),
+    (2, 64, 17, 260, 3, "zeros"),    # ragged H, W not a multiple of the 256-column wave tile
+    (1, 18, 8, 512, 4, "reflect"),   # two column tiles, cout 4, cin not a multiple of 4
+    (3, 5, 3, 68, 3, "zeros"),       # 3-row maps, 17 quads per row
+    (1, 64, 2, 8, 4, "reflect"),     # smallest reflect-padded map
+]
+
+
+@pytest.mark.parametrize("case", SMALLC_CASES)
+def test_conv3x3_smallc_streaming_bit_identical(case, hip_device):
+    """configs 36 / 37 (register-streaming direct conv, cout <= 4) against the oracle and bit-identical
+    to configs 10 / 11 (LDS-staged), which sum every output in the same tap-major, channel-minor order."""
+    n, cin, h, w, cout, pad = case
+    x = torch.from_numpy(synth.image(400 + cin, (n, cin, h, w)) * 2 - 0.5)
+    wt = torch.from_numpy(synth.conv_weight(500 + cin, cout, cin, 3))
+    bs = torch.from_numpy(synth.conv_bias(600 + cin, cout))
+    pre_r, act_r, _ = oracle_conv(x, wt, bs, 1, pad, False, True)
+    xd, wp, bd = x.to(hip_device), ops.pack_conv3x3(wt.to(hip_device)), bs.to(hip_device)
+    old = ops.conv3x3(xd, wp, bd, cout, pad_mode=pad, want_pre=True, want_act=True, cfg=10 if cout <= 3 else 11)
+    new = ops.conv3x3(xd, wp, bd, cout, pad_mode=pad, want_pre=True, want_act=True, cfg=36 if cout <= 3 else 37)
+    assert rel_inf(new[0], pre_r) <= OP_TOL
+    assert rel_inf(new[1], act_r) <= OP_TOL
+    assert torch.equal(new[0], old[0]) and torch.equal(new[1], old[1])
+    # the content|style pair input (x2) of the encoder path
+    half = n // 2
+    if half:
+        pair = ops.conv3x3(xd[:half], wp, bd, cout, pad_mode=pad, want_pre=True, want_act=False, x2=xd[half:],
+                           cfg=36 if cout <= 3 else 37)
+        assert torch.equal(pair[0], new[0])
