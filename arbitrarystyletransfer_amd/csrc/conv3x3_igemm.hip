@@ -1519,7 +1519,7 @@ __global__ __launch_bounds__(256, 3) void conv3x3_smallc_kernel(ConvArgs a) {
 // input channel each lane loads its 4 source rows as one 16-byte piece each, takes the columns left
 // and right of its piece from the neighbouring lanes (the wave's edge lanes and the image borders
 // load theirs), and accumulates 2 rows x 4 pixels x COUT outputs over the 9 taps (weights: one LDS
-// broadcast float4 per tap). The next channel's rows are in flight during the current channel's
+// broadcast float4 per tap). The next two channels' rows are in flight during the current channel's
 // FMAs. Same tap-major, channel-minor FMA order per output as conv3x3_smallc_kernel: bit-identical.
 // The smallc form stages 4-channel chunks in LDS behind two barriers each and ran at ~2 TB/s of its
 // input (latency-bound, 8x64x512^2 -> 3: 0.27 ms); this one streams.
@@ -1556,8 +1556,9 @@ __global__ __launch_bounds__(256) void conv3x3_smallc2_kernel(ConvArgs a) {
     for (int co = 0; co < COUT; ++co)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][co][j] = 0.f;
-  float4 cen[4];
-  float el[4], er[4];
+  // three channel buffers: channels c + 1 and c + 2 are in flight while channel c is computed
+  float4 cen[3][4];
+  float el[3][4], er[3][4];
   auto load = [&](int c, float4 (&cv)[4], float (&l)[4], float (&r)[4]) {
     const float* xc = xin + (int64_t)c * plane;
 #pragma unroll
@@ -1569,21 +1570,17 @@ __global__ __launch_bounds__(256) void conv3x3_smallc2_kernel(ConvArgs a) {
       r[k] = (ok && own_r && xr >= 0) ? row[xr] : 0.f;
     }
   };
-  load(0, cen, el, er);
-  for (int c = 0; c < Cin; ++c) {
-    float4 ncen[4];
-    float nel[4], ner[4];
-    if (c + 1 < Cin) load(c + 1, ncen, nel, ner);
+  auto compute = [&](int c, const float4 (&cv)[4], const float (&l)[4], const float (&r)[4]) {
     float v[4][6];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float left = __shfl_up(cen[k].w, 1, 64), right = __shfl_down(cen[k].x, 1, 64);
-      v[k][0] = own_l ? el[k] : left;
-      v[k][1] = cen[k].x;
-      v[k][2] = cen[k].y;
-      v[k][3] = cen[k].z;
-      v[k][4] = cen[k].w;
-      v[k][5] = own_r ? er[k] : right;
+      const float left = __shfl_up(cv[k].w, 1, 64), right = __shfl_down(cv[k].x, 1, 64);
+      v[k][0] = own_l ? l[k] : left;
+      v[k][1] = cv[k].x;
+      v[k][2] = cv[k].y;
+      v[k][3] = cv[k].z;
+      v[k][4] = cv[k].w;
+      v[k][5] = own_r ? r[k] : right;
     }
     const float4* wc = reinterpret_cast<const float4*>(Wsm + c * 36);
 #pragma unroll
@@ -1599,12 +1596,16 @@ __global__ __launch_bounds__(256) void conv3x3_smallc2_kernel(ConvArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][co][j] = fmaf(v[i + ky][j + kx], wco[co], acc[i][co][j]);
       }
-    if (c + 1 < Cin) {
+  };
+  load(0, cen[0], el[0], er[0]);
+  if (Cin > 1) load(1, cen[1], el[1], er[1]);
+  for (int c0 = 0; c0 < Cin; c0 += 3) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        cen[k] = ncen[k];
-        el[k] = nel[k];
-        er[k] = ner[k];
+    for (int u = 0; u < 3; ++u) {  // buffer u holds channel c0 + u
+      const int c = c0 + u;
+      if (c < Cin) {
+        if (c + 2 < Cin) load(c + 2, cen[(u + 2) % 3], el[(u + 2) % 3], er[(u + 2) % 3]);
+        compute(c, cen[u], el[u], er[u]);
       }
     }
   }
