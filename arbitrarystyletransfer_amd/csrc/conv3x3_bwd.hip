@@ -303,6 +303,143 @@ __global__ void relu_mask_kernel(const float* __restrict__ g, const float* __res
     out[i] = mask[i] > 0.f ? g[i] : 0.f;
 }
 
+// Input-gradient epilogue outside the conv (configurations without it: ops.conv3x3_dgrad's fallback):
+// dx[p][r][c] = epi(up == 2 ? the 2x2 window sum of raw (row by row) : raw[p][r][c]) with
+// epi(v) = mask > 0 ? add_post + (v + add_pre) : add_post -- conv3x3_igemm.hip's dgrad_epi_one.
+__global__ void dgrad_finish_kernel(const float* __restrict__ raw, float* __restrict__ dx, const float* __restrict__ mask,
+                                    const float* __restrict__ add_pre, const float* __restrict__ add_post,
+                                    int64_t planes, int h, int w, int up) {
+  const int64_t total = planes * h * w;
+  const int W = w * up;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % w);
+    const int64_t pr = i / w;  // plane * h + r
+    float v;
+    if (up == 2) {
+      const float* r0 = raw + (2 * pr) * W + 2 * c;
+      v = ((r0[0] + r0[1]) + r0[W]) + r0[W + 1];
+    } else {
+      v = raw[i];
+    }
+    if (add_pre) v = v + add_pre[i];
+    const bool keep = !mask || mask[i] > 0.f;
+    dx[i] = add_post ? (keep ? add_post[i] + v : add_post[i]) : (keep ? v : 0.f);
+  }
+}
+
+// Reflect-pad border of the input gradient (DecoderConvFn, ReflectionPad2d(1) after an optional x2
+// nearest upsample, models.py:598-628). The input-gradient conv computes the interior of the
+// padded-input gradient dP (a zero-padded same conv of dy); the reflect pad's adjoint also folds
+// dP's four border lines onto the source. With U = upsample(x) [H = h up, W = w up], dy [cout, H, W]:
+//   line 0  dP[ci][0][q]   = sum_{co, kx} w[co][ci][0][kx] dy[co][0][q - kx]      (-> U row 1)
+//   line 1  dP[ci][H+1][q] = sum_{co, kx} w[co][ci][2][kx] dy[co][H-1][q - kx]    (-> U row H - 2)
+//   line 2  dP[ci][p][0]   = sum_{co, ky} w[co][ci][ky][0] dy[co][p - ky][0]      (-> U col 1)
+//   line 3  dP[ci][p][W+1] = sum_{co, ky} w[co][ci][ky][2] dy[co][p - ky][W - 1]  (-> U col W - 2)
+// -- each a 1-D 3-tap correlation of a dy line (length L = W or H) over all cout, output length L + 2.
+// Pass 1 (border_lines_kernel) computes the four lines into a workspace [n][4][cin][Lmax + 2] as small
+// LDS-tiled GEMMs (workgroup: 32 ci x 64 positions, cout in chunks of 32); pass 2
+// (border_fold_kernel) gives each x element any line lands on one thread, which sums its
+// contributions in a fixed order and adds them, ReLU-masked like the interior, to dx: one writer
+// per element, no atomics.
+constexpr int BL_CI = 32, BL_Q = 64, BL_CO = 32;
+
+__global__ __launch_bounds__(256) void border_lines_kernel(const float* __restrict__ dy, const float* __restrict__ wt,
+                                                           float* __restrict__ lines, int cout, int cin, int H, int W,
+                                                           int Lp) {
+  __shared__ float Ds[BL_CO][BL_Q + 2];
+  __shared__ float Ws[BL_CO][BL_CI][3];
+  const int line = blockIdx.z & 3, n = blockIdx.z >> 2;
+  const int q0 = blockIdx.x * BL_Q, ci0 = blockIdx.y * BL_CI;
+  const bool row = line < 2;
+  const int L = row ? W : H;
+  if (q0 >= L + 2) return;
+  const int64_t plane = (int64_t)H * W;
+  // line start and element stride in a dy plane; the fixed tap of the other axis
+  const int64_t base = row ? (line == 0 ? 0 : (int64_t)(H - 1) * W) : (line == 2 ? 0 : W - 1);
+  const int stride = row ? 1 : W;
+  const int fixed = (line & 1) ? 2 : 0;
+  const float* dyn = dy + (int64_t)n * cout * plane + base;
+  const int t = threadIdx.x, ci = t >> 3, qg = t & 7;
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  for (int c0 = 0; c0 < cout; c0 += BL_CO) {
+    __syncthreads();
+    for (int e = t; e < BL_CO * (BL_Q + 2); e += 256) {
+      const int co = e / (BL_Q + 2), j = e - co * (BL_Q + 2), src = q0 - 2 + j;
+      Ds[co][j] = (c0 + co < cout && src >= 0 && src < L) ? dyn[(int64_t)(c0 + co) * plane + (int64_t)src * stride] : 0.f;
+    }
+    for (int e = t; e < BL_CO * BL_CI * 3; e += 256) {
+      const int co = e / (BL_CI * 3), r = e - co * (BL_CI * 3), cc = r / 3, k = r - 3 * cc;
+      // w[co][ci][ky][kx]: rows vary kx at ky = fixed, columns vary ky at kx = fixed
+      const int tap = row ? 3 * fixed + k : 3 * k + fixed;
+      Ws[co][cc][k] = (c0 + co < cout && ci0 + cc < cin) ? wt[((int64_t)(c0 + co) * cin + ci0 + cc) * 9 + tap] : 0.f;
+    }
+    __syncthreads();
+    const int cn = min(BL_CO, cout - c0);
+    for (int co = 0; co < cn; ++co) {
+      const float w0 = Ws[co][ci][0], w1 = Ws[co][ci][1], w2 = Ws[co][ci][2];
+      float dv[10];
+#pragma unroll
+      for (int j = 0; j < 10; ++j) dv[j] = Ds[co][8 * qg + j];
+      // dP[q] = sum_k w[k] D[q - k]; Ds[j] = D[q0 - 2 + j], q = q0 + 8 qg + i -> j = 8 qg + i + 2 - k
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = fmaf(w2, dv[i], fmaf(w1, dv[i + 1], fmaf(w0, dv[i + 2], acc[i])));
+    }
+  }
+  if (ci0 + ci >= cin) return;
+  float* out = lines + (((int64_t)n * 4 + line) * cin + ci0 + ci) * Lp;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int q = q0 + 8 * qg + i;
+    if (q < L + 2) out[q] = acc[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void border_fold_kernel(const float* __restrict__ lines, float* __restrict__ dx,
+                                                          const float* __restrict__ mask, int cin, int h, int w, int up,
+                                                          int Lp, int targets) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= targets) return;
+  const int pl = blockIdx.y;  // n * cin + ci
+  const int n = pl / cin, ci = pl - n * cin;
+  const int H = h * up, W = w * up;
+  // x rows / cols the four border lines land on
+  const int rt = 1 / up, rb = (H - 2) / up, ct = 1 / up, cr = (W - 2) / up;
+  const int nrow = rb != rt ? 2 : 1;
+  int r, c;
+  if (t < nrow * w) {
+    r = t < w ? rt : rb;
+    c = t < w ? t : t - w;
+  } else {
+    const int hr = h - nrow, t2 = t - nrow * w, side = t2 / hr;
+    r = t2 - side * hr;  // the r-th row that is neither rt nor rb
+    const int lo = min(rt, rb), hi = max(rt, rb);
+    if (r >= lo) ++r;
+    if (nrow == 2 && r >= hi) ++r;
+    c = side == 0 ? ct : cr;
+  }
+  const float* ln = lines + ((int64_t)n * 4 * cin + ci) * Lp;
+  const int64_t ls = (int64_t)cin * Lp;  // line stride
+  // padded columns q whose source column lands on x column c: U columns up c .. up c + up - 1
+  // (q = u + 1), plus the border columns
+  int qs[4], nq = 0;
+  for (int k = 0; k < up; ++k) qs[nq++] = up * c + k + 1;
+  if (c == ct) qs[nq++] = 0;
+  if (c == cr) qs[nq++] = W + 1;
+  float s = 0.f;
+  if (r == rt)
+    for (int k = 0; k < nq; ++k) s += ln[qs[k]];
+  if (r == rb)
+    for (int k = 0; k < nq; ++k) s += ln[ls + qs[k]];
+  if (c == ct)
+    for (int k = 0; k < up; ++k) s += ln[2 * ls + up * r + k + 1];
+  if (c == cr)
+    for (int k = 0; k < up; ++k) s += ln[3 * ls + up * r + k + 1];
+  const int64_t off = (int64_t)pl * h * w + (int64_t)r * w + c;
+  if (!mask || mask[off] > 0.f) dx[off] = dx[off] + s;
+}
+
 // ------------------------------------------------------------------------------------------
 // Weight gradient.
 // ------------------------------------------------------------------------------------------
@@ -980,6 +1117,44 @@ int ast_grad_pad_f32(const float* g, const float* mask, float* out_pad, long lon
   }
   hipLaunchKernelGGL(pad_grad_kernel, dim3(grid1(planes * (h + 2) * pitch)), dim3(256), 0, (hipStream_t)stream, g,
                      mask, out_pad, (int64_t)planes, h, w, pitch);
+  return (int)hipGetLastError();
+}
+
+int ast_dgrad_finish_f32(const float* raw, float* dx, const float* mask, const float* add_pre, const float* add_post,
+                         long long planes, int h, int w, int upsample, void* stream) {
+  if (!raw || !dx) return AST_E_NULLPTR;
+  if (planes <= 0 || h <= 0 || w <= 0) return AST_E_SHAPE;
+  if (upsample != 1 && upsample != 2) return AST_E_UNSUPPORTED;
+  hipLaunchKernelGGL(dgrad_finish_kernel, dim3(grid1(planes * h * w)), dim3(256), 0, (hipStream_t)stream, raw, dx, mask,
+                     add_pre, add_post, (int64_t)planes, h, w, upsample);
+  return (int)hipGetLastError();
+}
+
+long long ast_dgrad_reflect_border_workspace_floats(int n, int cin, int h, int w_in, int upsample) {
+  if (n <= 0 || cin <= 0 || h <= 0 || w_in <= 0 || (upsample != 1 && upsample != 2)) return 0;
+  return (long long)n * 4 * cin * (std::max(h, w_in) * upsample + 2);
+}
+
+int ast_dgrad_reflect_border_f32(const float* dy, const float* w, float* dx, const float* mask, float* workspace,
+                                 long long workspace_floats, int n, int cout, int cin, int h, int w_in, int upsample,
+                                 void* stream) {
+  if (!dy || !w || !dx || !workspace) return AST_E_NULLPTR;
+  if (n <= 0 || cout <= 0 || cin <= 0 || h <= 0 || w_in <= 0) return AST_E_SHAPE;
+  if (upsample != 1 && upsample != 2) return AST_E_UNSUPPORTED;
+  if (h * upsample < 2 || w_in * upsample < 2) return AST_E_SHAPE;  // ReflectionPad2d(1) needs size >= 2
+  if ((int64_t)n * cin >= 65536 || (int64_t)n * 4 >= 65536 || (int64_t)cout * h * w_in * upsample * upsample >= ((int64_t)1 << 31))
+    return AST_E_SHAPE;
+  if (workspace_floats < ast_dgrad_reflect_border_workspace_floats(n, cin, h, w_in, upsample)) return AST_E_SHAPE;
+  const int H = h * upsample, W = w_in * upsample, Lp = std::max(H, W) + 2;
+  hipLaunchKernelGGL(border_lines_kernel, dim3((Lp + BL_Q - 1) / BL_Q, (cin + BL_CI - 1) / BL_CI, n * 4), dim3(256), 0,
+                     (hipStream_t)stream, dy, w, workspace, cout, cin, H, W, Lp);
+  int e = (int)hipGetLastError();
+  if (e) return e;
+  const int rt = 1 / upsample, rb = (H - 2) / upsample, ct = 1 / upsample, cr = (W - 2) / upsample;
+  const int nrow = rb != rt ? 2 : 1, ncol = cr != ct ? 2 : 1;
+  const int targets = nrow * w_in + (h - nrow) * ncol;
+  hipLaunchKernelGGL(border_fold_kernel, dim3((targets + 255) / 256, n * cin), dim3(256), 0, (hipStream_t)stream,
+                     workspace, dx, mask, cin, h, w_in, upsample, Lp, targets);
   return (int)hipGetLastError();
 }
 

@@ -47,7 +47,40 @@ struct ConvArgs {
   int cin_pad, cout_pad;
   int reflect;  // 0: zero pad, 1: reflect pad (of the upsampled grid)
   int tiles_x, tiles_y;
+  // input-gradient epilogue (x3 kernels only; ast_conv3x3_dgrad_f32): with v the conv output at an
+  // output position (of y_pre, or of y_pool when e_sum2), v = v + e_add_pre; then
+  // v = e_mask > 0 ? e_add_post + v : e_add_post (the ReLU backward of the layer below, with its
+  // pre-ReLU tap gradient; a missing add_post reads as 0, a missing mask as > 0)
+  const float* e_mask;
+  const float* e_add_pre;
+  const float* e_add_post;
+  int e_sum2;  // y_pool holds the 2x2 SUM of the output (nearest-upsample adjoint), no ReLU / max
 };
+
+__device__ __forceinline__ bool dgrad_epi(const ConvArgs& a) { return a.e_mask || a.e_add_pre || a.e_add_post; }
+
+// the input-gradient epilogue of one output value at flat offset off (see ConvArgs)
+__device__ __forceinline__ float dgrad_epi_one(const ConvArgs& a, float v, int64_t off) {
+  if (a.e_add_pre) v = v + a.e_add_pre[off];
+  const bool keep = !a.e_mask || a.e_mask[off] > 0.f;
+  if (a.e_add_post) return keep ? a.e_add_post[off] + v : a.e_add_post[off];
+  return keep ? v : 0.f;
+}
+
+__device__ __forceinline__ float4 dgrad_epi4(const ConvArgs& a, float4 v, int64_t off) {
+  if (a.e_add_pre) {
+    const float4 u = *reinterpret_cast<const float4*>(a.e_add_pre + off);
+    v = make_float4(v.x + u.x, v.y + u.y, v.z + u.z, v.w + u.w);
+  }
+  float4 m = make_float4(1.f, 1.f, 1.f, 1.f), p = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.e_mask) m = *reinterpret_cast<const float4*>(a.e_mask + off);
+  if (a.e_add_post) {
+    p = *reinterpret_cast<const float4*>(a.e_add_post + off);
+    return make_float4(m.x > 0.f ? p.x + v.x : p.x, m.y > 0.f ? p.y + v.y : p.y, m.z > 0.f ? p.z + v.z : p.z,
+                       m.w > 0.f ? p.w + v.w : p.w);
+  }
+  return make_float4(m.x > 0.f ? v.x : 0.f, m.y > 0.f ? v.y : 0.f, m.z > 0.f ? v.z : 0.f, m.w > 0.f ? v.w : 0.f);
+}
 
 constexpr int kCinAlign = 8;    // packed cin padding (>= every CK)
 constexpr int kCoutAlign = 64;  // packed cout padding
@@ -573,6 +606,11 @@ __device__ __forceinline__ void store_region(const ConvArgs& a, const float* __r
       const int64_t off = ((int64_t)n * a.Cout + co) * plane + (int64_t)yy * W + xx;
       const bool full = vec4 && xx + 3 < W;
       const float vv[4] = {v.x, v.y, v.z, v.w};
+      if (dgrad_epi(a)) {  // input gradient: y_pre only
+        if (full) *reinterpret_cast<float4*>(a.y_pre + off) = dgrad_epi4(a, v, off);
+        else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_pre[off + r] = dgrad_epi_one(a, vv[r], off + r);
+        continue;
+      }
       if (a.y_pre) {
         if (full) *reinterpret_cast<float4*>(a.y_pre + off) = v;
         else for (int r = 0; r < 4; ++r) if (xx + r < W) a.y_pre[off + r] = vv[r];
@@ -593,10 +631,17 @@ __device__ __forceinline__ void store_region(const ConvArgs& a, const float* __r
       if (co >= a.Cout || py >= Ho || px >= Wo) continue;
       const float4 r0 = *reinterpret_cast<const float4*>(region + (ch * RM + 2 * prow) * RP + 4 * q);
       const float4 r1 = *reinterpret_cast<const float4*>(region + (ch * RM + 2 * prow + 1) * RP + 4 * q);
-      const float m0 = max_nan(relu_f(r0.x), relu_f(r1.x)), m1 = max_nan(relu_f(r0.y), relu_f(r1.y));
-      const float m2 = max_nan(relu_f(r0.z), relu_f(r1.z)), m3 = max_nan(relu_f(r0.w), relu_f(r1.w));
-      const float p0 = max_nan(m0, m1), p1 = max_nan(m2, m3);
       const int64_t off = ((int64_t)n * a.Cout + co) * Ho * Wo + (int64_t)py * Wo + px;
+      float p0, p1;
+      if (a.e_sum2) {  // nearest-upsample adjoint: the window's sum, row by row (pad_up_adjoint's order)
+        p0 = dgrad_epi_one(a, ((r0.x + r0.y) + r1.x) + r1.y, off);
+        p1 = px + 1 < Wo ? dgrad_epi_one(a, ((r0.z + r0.w) + r1.z) + r1.w, off + 1) : 0.f;
+      } else {
+        const float m0 = max_nan(relu_f(r0.x), relu_f(r1.x)), m1 = max_nan(relu_f(r0.y), relu_f(r1.y));
+        const float m2 = max_nan(relu_f(r0.z), relu_f(r1.z)), m3 = max_nan(relu_f(r0.w), relu_f(r1.w));
+        p0 = max_nan(m0, m1);
+        p1 = max_nan(m2, m3);
+      }
       if (px + 1 < Wo && (Wo & 1) == 0) {
         *reinterpret_cast<float2*>(a.y_pool + off) = make_float2(p0, p1);
       } else {
@@ -1743,6 +1788,14 @@ __global__ __launch_bounds__(TH * 32, OCC) void conv3x3_cin4_kernel(ConvArgs a, 
         u[j] = relu_f(o[j]);
       }
       const int64_t off = obase + (int64_t)co * plane;
+      if (a.y_pre && dgrad_epi(a)) {  // input gradient (ast_conv3x3_dgrad_f32): y_pre only
+        if (full) {
+          *reinterpret_cast<float4*>(a.y_pre + off) = dgrad_epi4(a, make_float4(o[0], o[1], o[2], o[3]), off);
+        } else {
+          for (int j = 0; j < 4; ++j) if (xx + j < W) a.y_pre[off + j] = dgrad_epi_one(a, o[j], off + j);
+        }
+        continue;
+      }
       if (a.y_pre) {
         if (full) {
           *reinterpret_cast<float4*>(a.y_pre + off) = make_float4(o[0], o[1], o[2], o[3]);
@@ -2104,6 +2157,39 @@ int ast_conv3x3_fwd_f32_cfg(int cfg, const float* x, const float* x2, int n2, co
   a.cout_pad = round_up(cout, kCoutAlign);
   a.reflect = pad_mode;
   return e.fn(a, (hipStream_t)stream, upsample);
+}
+
+int ast_conv3x3_dgrad_f32(int cfg, const float* dy, const float* w_tf_packed, float* dx, const float* mask,
+                          const float* add_pre, const float* add_post, int n, int cout, int h, int w, int cin,
+                          int upsample, void* stream) {
+  if (!dy || !w_tf_packed || !dx) return AST_E_NULLPTR;
+  if (n <= 0 || cout <= 0 || h <= 0 || w <= 0 || cin <= 0) return AST_E_SHAPE;
+  if (upsample != 1 && upsample != 2) return AST_E_UNSUPPORTED;
+  if (upsample == 2 && ((h | w) & 1)) return AST_E_SHAPE;  // the upsampled grid has even sides
+  if ((int64_t)cout * h * w >= ((int64_t)1 << 31)) return AST_E_SHAPE;
+  if ((int64_t)round_up(cout, kCinAlign) * 9 * round_up(cin, kCoutAlign) >= ((int64_t)1 << 31)) return AST_E_SHAPE;
+  const bool sum2 = upsample == 2;
+  if (cfg < 0) cfg = auto_config(cout, cin, n, h, w, 1, sum2, false);
+  // the epilogue is in the split-bf16 kernels (24-35) and, without the 2x2 sum, the cin <= 4 kernels (18-23)
+  if (!((cfg >= 24 && cfg <= 35) || (cfg >= 18 && cfg <= 23 && !sum2)) || cfg >= kNumConfigs) return AST_E_UNSUPPORTED;
+  static const int m16 = [] {
+    const char* v = getenv("AST_CONV_M16");
+    return v ? atoi(v) : 1;
+  }();
+  if (cfg >= 24 && cfg <= 27 && m16 == 1) cfg += 4;
+  if (cfg >= 28 && cfg <= 31 && m16 == 0) cfg -= 4;
+  const CfgEntry& e = kConfigs[cfg];
+  if (sum2 && e.rm % 2 != 0) return AST_E_UNSUPPORTED;
+  if (e.bn > kCoutAlign && (cin % e.bn) != 0) return AST_E_UNSUPPORTED;
+  ConvArgs a{};
+  a.x = dy; a.nsplit = n; a.wp = w_tf_packed;
+  (sum2 ? a.y_pool : a.y_pre) = dx;
+  a.e_mask = mask; a.e_add_pre = add_pre; a.e_add_post = add_post; a.e_sum2 = sum2 ? 1 : 0;
+  a.N = n; a.Cin = cout; a.Hin = h; a.Win = w; a.Cout = cin; a.H = h; a.W = w;
+  a.cin_pad = round_up(cout, kCinAlign);
+  a.cout_pad = round_up(cin, kCoutAlign);
+  a.reflect = 0;  // the interior of the padded-input gradient: a zero-padded same conv of dy
+  return e.fn(a, (hipStream_t)stream, 1);
 }
 
 int ast_conv3x3_fwd_f32(const float* x, const float* w_packed, const float* bias, float* y_pre, float* y_act,

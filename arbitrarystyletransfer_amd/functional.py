@@ -59,6 +59,59 @@ def conv_input_grad_same(dy, weight, in_scale=None):
     return pre
 
 
+_E_UNSUPPORTED = -3  # AST_E_UNSUPPORTED (include/ast_hip.h)
+
+
+def conv_input_grad(dy, weight, upsample=1, pad_mode="zeros", in_scale=None, mask=None, add_pre=None,
+                    add_post=None):
+    """dL/dx of y = conv3x3(pad(upsample(x))) given dL/dy, with the fused input-gradient epilogue of
+    ast_conv3x3_dgrad_f32: dx = mask > 0 ? add_post + (g + add_pre) : add_post (mask = the ReLU
+    output feeding this conv: the ReLU backward of the layer below; add_pre / add_post = gradient
+    taps of that layer's ReLU output / pre-ReLU output; each optional). Reflect padding: the
+    border fold (ast_dgrad_reflect_border_f32) after the interior. Configurations without the
+    fused epilogue (small packed planes, cin < 16 after the swap) run the plain input-gradient conv
+    and the same epilogue as one elementwise pass (identical arithmetic per element)."""
+    dy = _dev(dy, "dy")
+    cout, cin = int(weight.shape[0]), int(weight.shape[1])
+    n, _, H, W = (int(v) for v in dy.shape)
+    up = int(upsample)
+    h, w = H // up, W // up
+    ext = []
+    for t, name in ((mask, "mask"), (add_pre, "add_pre"), (add_post, "add_post")):
+        if t is not None:
+            t = _dev(t, name)
+            if tuple(t.shape) != (n, cin, h, w):
+                raise HipOpError(f"{name} {tuple(t.shape)} must be the input's shape {(n, cin, h, w)}")
+        ext.append(t)
+    mask, add_pre, add_post = ext
+    if pad_mode == "reflect" and in_scale is not None:
+        raise HipOpError("in_scale (the conv_1 normalisation) comes with zero padding only")
+    if up == 1 and mask is None and add_pre is None and add_post is None:
+        dx = conv_input_grad_same(dy, weight, in_scale)
+    else:
+        dx = _empty((n, cin, h, w), dy)
+        code = _E_UNSUPPORTED
+        if ops.pack_plan(n, W, False) == (1, 0):
+            packed = _TF.get(weight, in_scale)
+            cfg = ops.tuned_config(n, cout, H, W, cin, 1, "zeros", up == 2)
+            code = ops._timed(f"conv3x3 dgrad {cout}->{cin} {H}x{W} up{up}", 2 * n * H * W * cout * cin * 9, dy.device,
+                              lambda: lib().ast_conv3x3_dgrad_f32(cfg, ptr(dy), ptr(packed), ptr(dx), ptr(mask),
+                                                                  ptr(add_pre), ptr(add_post), n, cout, H, W, cin,
+                                                                  up, _s(dy)))
+        if code == _E_UNSUPPORTED:
+            raw = conv_input_grad_same(dy, weight, in_scale)
+            check(lib().ast_dgrad_finish_f32(ptr(raw), ptr(dx), ptr(mask), ptr(add_pre), ptr(add_post), n * cin, h, w,
+                                             up, _s(dy)), "dgrad_finish")
+        else:
+            check(code, "conv3x3_dgrad")
+    if pad_mode == "reflect":
+        wt = _dev(weight.detach(), "weight")
+        ws = workspace(lib().ast_dgrad_reflect_border_workspace_floats(n, cin, h, w, up), dy.device)
+        check(lib().ast_dgrad_reflect_border_f32(ptr(dy), ptr(wt), ptr(dx), ptr(mask), ptr(ws), ws.numel(), n, cout,
+                                                 cin, h, w, up, _s(dy)), "dgrad_reflect_border")
+    return dx
+
+
 # id(parameter) -> dp.FlatGradArena: weight gradients are written straight into the arena slice
 # (a view, which autograd adopts as .grad without copying).
 GRAD_ARENA = {}
@@ -141,6 +194,84 @@ class EncoderConvFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None, None
 
 
+class LossNetFn(torch.autograd.Function):
+    """The whole frozen VGG walk of PretrainedEncoder (models.py:226-240) as one autograd node, so
+    its backward sees every tap gradient at once and can fuse across layers: the ReLU backward of a
+    layer not followed by a max-pool runs in the next layer's input-gradient epilogue (mask = that
+    conv's input, the ReLU output; the layer's relu_i / conv_i tap gradients as add_pre / add_post,
+    conv_input_grad), instead of a separate ast_conv_act_backward_f32 pass per layer. Layers under a
+    max-pool and the top layer keep that pass (it routes the pooled gradient). Same arithmetic per
+    element as the per-layer EncoderConvFn chain. Used when no conv parameter needs a gradient
+    (the loss network of every trainer); forward outputs: the requested taps in network order."""
+
+    @staticmethod
+    def forward(ctx, net, x):
+        ctx.set_materialize_grads(False)
+        norm = net._vgg_layers[0]
+        plan = net._plan()
+        outs, pres, ins = [], [], []
+        cur = x
+        for idx, conv, want_pre, want_act, want_pool, collect in plan:
+            first = idx == 1
+            pre, act, pool = ops.conv3x3(cur, net._packed.get(conv), conv.bias, conv.out_channels, pad_mode="zeros",
+                                         in_mean=norm.mean.view(-1) if first else None,
+                                         in_std=norm.std.view(-1) if first else None,
+                                         want_pre=True, want_act=want_act, want_pool=want_pool)
+            by_name = {conv.name: pre, f"relu_{idx}": act, f"pool_{idx}": pool}
+            outs.extend(by_name[nm] for nm in collect)
+            pres.append(pre)
+            ins.append(cur)
+            cur = pool if want_pool else act
+        ctx.plan = [(idx, conv, want_pool, collect) for idx, conv, _, _, want_pool, collect in plan]
+        ctx.std = norm.std.view(-1)
+        ctx.save_for_backward(*pres, *ins[1:])
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        saved = ctx.saved_tensors
+        L = len(ctx.plan)
+        pres, ins = saved[:L], (None,) + tuple(saved[L:])
+        taps, k = [], 0
+        for idx, conv, want_pool, collect in ctx.plan:
+            t = {}
+            for nm in collect:
+                t[nm.split("_")[0]] = grads[k]
+                k += 1
+            taps.append((t.get("conv"), t.get("relu"), t.get("pool")))
+
+        def act_backward(j, g_pool):
+            gp, ga, gq = taps[j]
+            if g_pool is not None:
+                gq = g_pool if gq is None else gq + g_pool
+            if gp is None and ga is None and gq is None:
+                return None
+            pre = pres[j]
+            n, c, h, w = pre.shape
+            dy = torch.empty_like(pre)
+            check(lib().ast_conv_act_backward_f32(ptr(pre), ptr(_dev(gp, "g") if gp is not None else None),
+                                                  ptr(_dev(ga, "g") if ga is not None else None),
+                                                  ptr(_dev(gq, "g") if gq is not None else None), ptr(dy),
+                                                  n * c, h, w, _s(pre)), "conv_act_backward")
+            return dy
+
+        dy = act_backward(L - 1, None)
+        for j in range(L - 1, 0, -1):
+            conv = ctx.plan[j][1]
+            pooled = ctx.plan[j - 1][2]
+            if dy is None:
+                dy = act_backward(j - 1, None)
+            elif pooled:
+                dy = act_backward(j - 1, conv_input_grad(dy, conv.weight))
+            else:
+                gp, ga, _ = taps[j - 1]
+                dy = conv_input_grad(dy, conv.weight, mask=ins[j], add_pre=ga, add_post=gp)
+        dx = None
+        if dy is not None and ctx.needs_input_grad[1]:
+            dx = conv_input_grad(dy, ctx.plan[0][1].weight, in_scale=ctx.std)
+        return None, dx
+
+
 def normalize_image(x, mean, std):
     x = _dev(x, "x")
     n, c = x.shape[:2]
@@ -157,14 +288,22 @@ def normalize_image(x, mean, std):
 # ------------------------------------------------------------------------------------------------
 
 class DecoderConvFn(torch.autograd.Function):
+    """[Upsample x2] -> ReflectionPad(1) -> conv3x3 -> [ReLU] (models.py:598-628).
+
+    Backward: dy = the output gradient (ReLU-masked here unless `out_premasked`), then the input
+    gradient with the reflect border fold (conv_input_grad) and the weight gradient on dense dy.
+    `mask_input`: the input is the ReLU output of the previous decoder layer and feeds only this
+    layer, so that layer's ReLU backward (input > 0) runs in this layer's input-gradient epilogue;
+    the previous layer is then built with `out_premasked` and passes its gradient through."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, packed, upsample, relu):
+    def forward(ctx, x, weight, bias, packed, upsample, relu, mask_input=False, out_premasked=False):
         pre, act, _ = ops.conv3x3(x, packed, bias, weight.shape[0], upsample=upsample, pad_mode="reflect",
                                   want_pre=not relu, want_act=relu)
         out = act if relu else pre
         ctx.save_for_backward(x, weight, out)
         ctx.upsample, ctx.relu, ctx.has_bias = upsample, relu, bias is not None
+        ctx.mask_input, ctx.out_premasked = bool(mask_input), bool(out_premasked)
         ctx.param_ids = (weight, bias)  # for the DP gradient arena lookup (not saved tensors)
         return out
 
@@ -173,23 +312,17 @@ class DecoderConvFn(torch.autograd.Function):
         x, weight, out = ctx.saved_tensors
         g = _dev(g, "grad")
         n, cout, H, W = out.shape
-        cin = x.shape[1]
-        # ReLU-masked output gradient, zero-padded by one pixel (pitch a multiple of 4 so the
-        # dgrad conv's vector gather applies): a same conv over it is the full padded-input grad
-        pitch = (W + 2 + 3) // 4 * 4
-        dyp = torch.empty((n, cout, H + 2, pitch), device=g.device, dtype=torch.float32)
-        check(lib().ast_grad_pad_f32(ptr(g), ptr(out) if ctx.relu else None, ptr(dyp), n * cout, H, W, pitch,
-                                     _s(g)), "grad_pad")
+        if ctx.relu and not ctx.out_premasked:
+            dy = torch.empty_like(g)
+            check(lib().ast_relu_mask_f32(ptr(g), ptr(out), ptr(dy), g.numel(), _s(g)), "relu_mask")
+        else:
+            dy = g
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dp = conv_input_grad_same(dyp, weight)          # [n, cin, H+2, pitch]
-            dx = torch.empty_like(x)
-            check(lib().ast_pad_up_adjoint_f32(ptr(dp), ptr(dx), n * cin, x.shape[2], x.shape[3], ctx.upsample,
-                                               pitch, _s(g)), "pad_up_adjoint")
+            dx = conv_input_grad(dy, weight, ctx.upsample, "reflect", mask=x if ctx.mask_input else None)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            dw, db = conv_weight_grad(x, dyp, cout, ctx.upsample, "reflect", ctx.has_bias, *ctx.param_ids,
-                                      dy_layout=(pitch, (H + 2) * pitch, pitch + 1))
-        return dx, dw, db, None, None, None
+            dw, db = conv_weight_grad(x, dy, cout, ctx.upsample, "reflect", ctx.has_bias, *ctx.param_ids)
+        return (dx, dw, db) + (None,) * (len(ctx.needs_input_grad) - 3)  # 6 or 8 inputs
 
 
 # ------------------------------------------------------------------------------------------------

@@ -275,7 +275,10 @@ class PretrainedEncoder(nn.Module):
 
     def _forward_autograd(self, x):
         """Same walk through EncoderConvFn (HIP forward + HIP backward; the pre-ReLU output is
-        always kept for the ReLU / max-pool backward)."""
+        always kept for the ReLU / max-pool backward); frozen weights: one LossNetFn node for the
+        whole walk (cross-layer fused backward)."""
+        if not any(p.requires_grad for p in self.parameters()):
+            return list(Fn.LossNetFn.apply(self, x))
         norm = self._vgg_layers[0]
         outs = []
         cur = x
@@ -340,8 +343,12 @@ class VGGDecoder(nn.Sequential):
                 x = act if relu else pre
             return x
         if _needs_grad(x, self):
-            for conv, up, relu in self._groups:
-                x = Fn.DecoderConvFn.apply(x, conv.weight, conv.bias, self._packed.get(conv), 2 if up else 1, relu)
+            # each ReLU output feeds only the next conv: its ReLU backward runs in that conv's
+            # input-gradient epilogue (mask_input), and the layer itself passes its gradient through
+            g = self._groups
+            for k, (conv, up, relu) in enumerate(g):
+                x = Fn.DecoderConvFn.apply(x, conv.weight, conv.bias, self._packed.get(conv), 2 if up else 1, relu,
+                                           k > 0 and g[k - 1][2], relu and k + 1 < len(g))
             return x
         for conv, up, relu in self._groups:
             pre, act, _ = ops.conv3x3(x, self._packed.get(conv), conv.bias, conv.out_channels,

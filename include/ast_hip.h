@@ -160,6 +160,38 @@ int ast_grad_pad_f32(const float* g, const float* mask, float* out_pad, long lon
 int ast_pad_up_adjoint_f32(const float* dp_full, float* dx, long long planes, int h_in, int w_in,
                            int upsample, int pitch, void* stream);
 
+/* Input gradient with a fused epilogue (round 5; replaces the grad_pad -> dgrad -> pad_up_adjoint
+ * chain of the decoder and the ReLU backward of the layer below, models.py:216-218, 598-628).
+ * For the forward y = conv3x3(pad(upsample(x))) with dy [n, cout, h, w] (h, w: the conv's output
+ * grid, = upsample x the source grid): dx [n, cin, h/up, w/up] = epi(S(D)) where D = the zero-padded
+ * same conv of dy with the transposed+flipped pack w_tf_packed (the interior of the padded-input
+ * gradient), S = the 2x2 window sum when upsample == 2 (the nearest-upsample adjoint), and
+ * epi(v) = mask > 0 ? add_post + (v + add_pre) : add_post per element of dx (mask, add_pre,
+ * add_post [n, cin, h/up, w/up], each optional: no mask keeps every element, no add_post reads 0).
+ * Reflect padding's border fold is ast_dgrad_reflect_border_f32, run after this.
+ * The epilogue is the split-bf16 kernels' (cfg 24-35) and, for upsample 1, the cout <= 4 direct
+ * kernels' (cfg 18-23; -1 = heuristic): AST_E_UNSUPPORTED for any other configuration -- the
+ * caller then runs ast_conv3x3_fwd_f32_cfg + ast_dgrad_finish_f32. */
+int ast_conv3x3_dgrad_f32(int cfg, const float* dy, const float* w_tf_packed, float* dx,
+                          const float* mask, const float* add_pre, const float* add_post, int n,
+                          int cout, int h, int w, int cin, int upsample, void* stream);
+
+/* The same epilogue as a separate pass over a plain input-gradient conv's output raw
+ * [planes, h*up, w*up]: dx [planes, h, w] = epi(S(raw)). */
+int ast_dgrad_finish_f32(const float* raw, float* dx, const float* mask, const float* add_pre,
+                         const float* add_post, long long planes, int h, int w, int upsample,
+                         void* stream);
+
+/* Reflect-pad border of the input gradient of conv3x3(ReflectionPad2d(1)(upsample(x))): adds to
+ * dx [n, cin, h, w_in] the padded-input gradient's four border lines (computed from dy [n, cout,
+ * h*up, w_in*up] and the forward filter w [cout, cin, 3, 3] into the workspace) folded as the
+ * reflect pad and upsample map them, masked like the interior (mask [n, cin, h, w_in] > 0, or
+ * NULL). workspace: ast_dgrad_reflect_border_workspace_floats floats. */
+long long ast_dgrad_reflect_border_workspace_floats(int n, int cin, int h, int w_in, int upsample);
+int ast_dgrad_reflect_border_f32(const float* dy, const float* w, float* dx, const float* mask,
+                                 float* workspace, long long workspace_floats, int n, int cout,
+                                 int cin, int h, int w_in, int upsample, void* stream);
+
 /* dw [cout, cin, 3, 3] = sum over images/pixels of dy x pad(upsample(x)) (overwritten; split-bf16
  * MFMA, split over pixel tiles: each split's partial dW/db goes to the workspace, then one ordered
  * reduce); db [cout] = sum of dy (optional). workspace: ast_conv3x3_wgrad_workspace_floats floats. */

@@ -1,6 +1,8 @@
 """Alternating A/B runs of one bench mode under different environments (variant libraries through
 AST_HIP_LIB, feature switches), each arm in a fresh process, ROUNDS rounds in interleaved order:
 python scripts/ab_runs.py MODE ROUNDS "name:VAR=val,VAR2=val" ["name2:..." ...]
+TREE=path (relative to the repo root) runs that arm's bench.py from another checkout (e.g. a git
+worktree of the previous commit with its own in-tree libraries): A/B of Python and kernels together.
 Prints per run: img/s, ms/step and the per-kernel-family ms/step of the bench line."""
 import json
 import os
@@ -22,8 +24,10 @@ def main():
         arms.append((name, kv))
     for rnd in range(rounds):
         for name, kv in (arms if rnd % 2 == 0 else arms[::-1]):
-            r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--mode", mode, "--cpu-seconds", "0",
-                                "--steps", "10", "--warmup", "3"], env=dict(os.environ, **kv), capture_output=True,
+            env = dict(os.environ, **kv)
+            tree = os.path.join(ROOT, env.pop("TREE")) if "TREE" in env else ROOT
+            r = subprocess.run([sys.executable, os.path.join(tree, "bench.py"), "--mode", mode, "--cpu-seconds", "0",
+                                "--steps", "10", "--warmup", "3"], env=env, cwd=tree, capture_output=True,
                                text=True, timeout=280)
             if r.returncode != 0:
                 print(name, "FAILED", r.stderr[-1500:], flush=True)

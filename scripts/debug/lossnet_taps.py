@@ -1,0 +1,52 @@
+"""Debug: LossNetFn vs the per-layer EncoderConvFn chain vs CPU float64, per tap set."""
+import sys
+import numpy as np
+import torch
+import torch.nn.functional as F
+sys.path.insert(0, ".")
+from arbitrarystyletransfer_amd import models, synth
+from oracle import ref_cpu as R
+
+d = torch.device("cuda:0")
+
+
+def rel(a, b):
+    a = a.detach().double().cpu(); b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max())
+
+
+def run(taps, H=64, W=48):
+    net = models.PretrainedEncoder(taps).to(d).eval().requires_grad_(False)
+    x = torch.from_numpy(synth.uniform(81, 2 * 3 * H * W).astype(np.float32).reshape(2, 3, H, W))
+    xr = x.double().requires_grad_()
+    cur = R.normalization(xr)
+    outs = {}
+    convs = net.convs()
+    k = 0
+    for v in synth.VGG19_CFG:
+        if v == "M":
+            cur = F.max_pool2d(cur, 2, 2); outs[f"pool_{k}"] = cur; continue
+        c = convs[k]; k += 1
+        pre = F.conv2d(cur, c.weight.detach().cpu().double(), c.bias.detach().cpu().double(), padding=1)
+        outs[f"conv_{k}"] = pre; cur = F.relu(pre); outs[f"relu_{k}"] = cur
+        if all(t in outs for t in taps):
+            break
+    gs = [torch.from_numpy((synth.uniform(90 + i, int(np.prod(outs[t].shape))) * 2 - 1).astype(np.float32)
+                           .reshape(outs[t].shape)) for i, t in enumerate(taps)]
+    sum((outs[t] * g.double()).sum() for t, g in zip(taps, gs)).backward()
+    res = []
+    for fused in (True, False):
+        net.requires_grad_(not fused)
+        xd = x.to(d).requires_grad_()
+        got = net(xd)
+        sum((o * g.to(d)).sum() for o, g in zip(got, gs)).backward()
+        res.append(rel(xd.grad, xr.grad))
+        if not fused:
+            net.zero_grad(set_to_none=True)
+    print(f"{str(taps):60s} fused {res[0]:.2e} chain {res[1]:.2e}", flush=True)
+
+
+for taps in [("relu_1",), ("relu_1", "relu_2"), ("relu_2",), ("conv_2",), ("relu_1", "conv_3"), ("relu_3",),
+             ("relu_3", "relu_4"), ("relu_5",), ("relu_5", "relu_6"), ("relu_9", "relu_10"), ("relu_13", "relu_14"),
+             ("relu_14", "relu_15"), tuple(f"relu_{i}" for i in range(1, 16))]:
+    run(taps)
