@@ -426,7 +426,8 @@ def gram(f, g, scale):
     b, c = int(f.shape[0]), int(f.shape[1])
     hw = f.numel() // (b * c)
     ws = workspace(lib().ast_gram_workspace_floats(b, c, hw), f.device)
-    check(lib().ast_gram_f32(ptr(f), ptr(g), b, c, hw, scale, ptr(ws), ws.numel(), _s(f)), "gram")
+    check(ops._timed(f"gram {c}x{hw}", 2 * b * c * c * hw, f.device,
+                     lambda: lib().ast_gram_f32(ptr(f), ptr(g), b, c, hw, scale, ptr(ws), ws.numel(), _s(f))), "gram")
 
 
 class GramFn(torch.autograd.Function):
@@ -543,8 +544,10 @@ class StyleLossFn(torch.autograd.Function):
         x, dg, ra, rb = ctx.saved_tensors
         b, c, h, w = x.shape
         dx = torch.empty_like(x)
-        check(lib().ast_gram_backward_f32(ptr(x), ptr(dg), ptr(dx), ptr(ra), ptr(rb), b, c, h * w, 1.0 / (c * h * w),
-                                          ptr(_dev(g, "grad")), 0, _s(x)), "gram_backward")
+        gg = _dev(g, "grad")
+        check(ops._timed(f"gram_bwd {c}x{h * w}", 2 * b * c * c * h * w, x.device,
+                         lambda: lib().ast_gram_backward_f32(ptr(x), ptr(dg), ptr(dx), ptr(ra), ptr(rb), b, c, h * w,
+                                                             1.0 / (c * h * w), ptr(gg), 0, _s(x))), "gram_backward")
         return dx, None, None
 
 

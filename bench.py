@@ -101,6 +101,9 @@ def train_bench(args, dev, rank, world):
     tf = fl / (ms * 1e-3) / 1e12
     wg = [(f, m) for tag, f, m in mm if tag.startswith("wgrad")]
     wg_tf = sum(f for f, _ in wg) / (sum(m for _, m in wg) * 1e-3) / 1e12 if wg else None
+    # every matrix-core kernel of the step: the convs and wgrads above plus the loss Gram matrices
+    # and their backward (v_mfma_f32_32x32x2f32, csrc/losses.hip)
+    ms_gram = sum(m for tag, _, m in recs if tag.startswith(("gram ", "gram_bwd ")))
     result = {
         "metric": "AdaIN training images/sec at 512x512 (config 3: bs=16/GPU; config 4: batch-sharded)",
         "value": B * world * args.steps / elapsed, "unit": "images/s", "n_gpus": world, "steps": args.steps,
@@ -117,6 +120,7 @@ def train_bench(args, dev, rank, world):
                      "fp32_mfma_peak": PEAK_FP32_MFMA_TF, "frac_of_fp32_mfma_peak": tf / PEAK_FP32_MFMA_TF,
                      "traffic": None, "wgrad_tflops": wg_tf,
                      "mfma_share_of_step": ms / args.steps / (elapsed / args.steps * 1e3),
+                     "matrix_kernels_share_of_step": (ms + ms_gram) / args.steps / (elapsed / args.steps * 1e3),
                      "mfma_tflop_per_step": fl / args.steps / 1e12},
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0 and not args.full_losses:
