@@ -715,7 +715,12 @@ __device__ unsigned x3_stamp_buf[kX3StampWgs * 16 * kX3StampRec];
 // higher clock with the 16x16 shape (MI355X_MICROARCH.md, DVFS give-back item 7). A lane's k-group
 // g = lane >> 4 selects the term plane (g < 2: the first, else the second) and the 8-channel half
 // (g & 1), so every operand is still one ds_read_b128 from the same LDS images.
-template <int WM, int RM, int RN, int UP, int OCC, bool M16 = false>
+// PER (M16 only): persistent form -- gridDim.x workgroups walk the blocks b = blockIdx.x + k gridDim.x
+// (gridDim.x a multiple of 8, so b % 8 and the XCD stay fixed), the same code per block; between
+// blocks an LDS-only barrier (the epilogue regions are read before the next prologue writes the
+// tiles), so the epilogue's global stores drain under the next block's prologue instead of
+// holding the CU until the workgroup retires.
+template <int WM, int RM, int RN, int UP, int OCC, bool M16 = false, bool PER = false>
 __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   using C = X3Cfg<WM, RM, RN, UP>;
   constexpr int NT = C::NT, TH = C::TH, BN = C::BN, SR = C::SR, SC = C::SC, A_PLANE = C::A_PLANE;
@@ -729,13 +734,28 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
   u32x4* Blo = x3_smem + C::A_UNITS;
   u32x4* Bhm0 = Blo + 18 * BN;
 
-  const int tid = threadIdx.x, wm = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
 #if X3_STAMP
   unsigned st0 = 0, st1 = 0, st2 = 0;
   X3_ST(0);
 #endif
+  static_assert(!PER || M16, "persistent form of the M16 kernel only");
+  const int ntl = a.tiles_x * a.tiles_y * a.N, ngr = (a.Cout + BN - 1) / BN;
+  const int nblk = (ntl + 7) / 8 * 8 * ngr;
+  for (int bid = blockIdx.x;; bid += gridDim.x) {
+  if constexpr (PER) {
+    if (bid >= nblk) break;
+    if (bid != (int)blockIdx.x) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  // PER: the thread index laundered per block, so nothing derived from it is hoisted out of the
+  // block loop and held live through it (that spilled 60-80 VGPRs); recomputing is a few VALU ops
+  int tid_ = threadIdx.x;
+  if constexpr (PER) asm volatile("" : "+v"(tid_));
+  const int tid = tid_, wm = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   int t, grp;
-  if (!decode_block(blockIdx.x, a.tiles_x * a.tiles_y * a.N, (a.Cout + BN - 1) / BN, t, grp)) return;
+  if (!decode_block(bid, ntl, ngr, t, grp)) {
+    if constexpr (PER) continue;
+    return;
+  }
   const int tx = t % a.tiles_x;
   t /= a.tiles_x;
   const int ty = t % a.tiles_y;
@@ -1119,6 +1139,8 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
     store_tiles<RM, RN>(a, acc, n, x0, y0, wm * RM, n0, h, l32);
 #endif
   }
+  if constexpr (!PER) break;
+  }  // block loop
 }
 
 // Persistent form of the M16 split-bf16 kernel (round 4). One workgroup per CU
@@ -1917,7 +1939,19 @@ int launch_cin4(const ConvArgs& a0, hipStream_t s, int up) {
   return (int)hipGetLastError();
 }
 
-template <int WM, int RM, int RN, int UP, int OCC, bool M16>
+int cu_count() {  // CUs of the current device (looked up on a device's first call)
+  static int cus_of[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int cus = dev >= 0 && dev < 64 ? cus_of[dev] : 0;
+  if (!cus) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (dev >= 0 && dev < 64) cus_of[dev] = cus;
+  }
+  return cus;
+}
+
+template <int WM, int RM, int RN, int UP, int OCC, bool M16, bool PER = false>
 int launch_x3_one(const ConvArgs& a0, hipStream_t s) {
   using C = X3Cfg<WM, RM, RN, UP>;
   ConvArgs a = a0;
@@ -1925,9 +1959,13 @@ int launch_x3_one(const ConvArgs& a0, hipStream_t s) {
   a.tiles_y = cdiv(a.H, C::TH);
   if (cdiv(a.Cout, C::BN) * C::BN > a.cout_pad) return AST_E_UNSUPPORTED;
   const int64_t ntiles = (int64_t)a.tiles_x * a.tiles_y * a.N;
-  const int64_t nblk = (ntiles + 7) / 8 * 8 * cdiv(a.Cout, C::BN);
+  int64_t nblk = (ntiles + 7) / 8 * 8 * cdiv(a.Cout, C::BN);
   if (nblk >= 0x7fffffff) return AST_E_SHAPE;
-  auto kern = conv3x3_x3_kernel<WM, RM, RN, UP, OCC, M16>;
+  if (PER) {  // one workgroup per CU slot, a multiple of 8 (the XCD of a block stays fixed)
+    const int64_t slots = (int64_t)(cu_count() + 7) / 8 * 8 * OCC;
+    nblk = nblk < slots ? nblk : slots;
+  }
+  auto kern = conv3x3_x3_kernel<WM, RM, RN, UP, OCC, M16, PER>;
   constexpr int lds = M16 ? C::LDS_BYTES_M16 : C::LDS_BYTES;
   static_assert(lds * OCC <= 160 * 1024, "LDS per CU");
   static bool attr_set = false;
@@ -1980,11 +2018,11 @@ int launch_x3p(const ConvArgs& a, hipStream_t s, int up) {
 }
 
 // split-bf16 MFMA kernel: no fused input normalisation (conv_1 runs the direct cin<=4 kernel)
-template <int WM, int RM, int RN, int OCC = 1, bool M16 = false>
+template <int WM, int RM, int RN, int OCC = 1, bool M16 = false, bool PER = false>
 int launch_x3(const ConvArgs& a, hipStream_t s, int up) {
   if (a.in_mean) return AST_E_UNSUPPORTED;
   if ((int64_t)a.Cin * a.Hin * a.Win * 4 >= ((int64_t)1 << 31)) return AST_E_UNSUPPORTED;  // 32-bit buffer offsets
-  return up == 2 ? launch_x3_one<WM, RM, RN, 2, OCC, M16>(a, s) : launch_x3_one<WM, RM, RN, 1, OCC, M16>(a, s);
+  return up == 2 ? launch_x3_one<WM, RM, RN, 2, OCC, M16, PER>(a, s) : launch_x3_one<WM, RM, RN, 1, OCC, M16, PER>(a, s);
 }
 
 struct CfgEntry {
@@ -2040,6 +2078,11 @@ const CfgEntry kConfigs[] = {
     // register-streaming direct VALU conv for cout <= 4 (no LDS tile, no per-channel barrier)
     {launch_smallc2<3>, 4, 8, 2, 3},                    // 36: cout <= 3
     {launch_smallc2<4>, 4, 8, 2, 4},                    // 37: cout <= 4
+    // persistent forms of 28-31 (round 5): the same kernel looping over blocks
+    {launch_x3<8, 2, 2, 1, true, true>, 64, 16, 2, 0},  // 38: as 28
+    {launch_x3<4, 2, 2, 1, true, true>, 64, 8, 2, 0},   // 39: as 29
+    {launch_x3<4, 2, 1, 2, true, true>, 32, 8, 2, 0},   // 40: as 30
+    {launch_x3<8, 2, 1, 1, true, true>, 32, 16, 2, 0},  // 41: as 31
 };
 constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -2144,6 +2187,7 @@ int ast_conv3x3_fwd_f32_cfg(int cfg, const float* x, const float* x2, int n2, co
     return v ? atoi(v) : 0;
   }();
   if (cfg >= 28 && cfg <= 31 && persist == 1) cfg += 4;
+  if (cfg >= 28 && cfg <= 31 && persist == 2) cfg += 10;  // AST_CONV_PERSIST=2: 38-41
   const CfgEntry& e = kConfigs[cfg];
   if (y_pool && (e.rm % 2 != 0 || e.max_cout)) return AST_E_UNSUPPORTED;
   if (e.max_cout && cout > e.max_cout) return AST_E_UNSUPPORTED;

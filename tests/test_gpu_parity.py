@@ -111,8 +111,9 @@ PERSIST_CASES = [
 @pytest.mark.parametrize("case", PERSIST_CASES)
 def test_conv3x3_persistent_bit_identical(case, hip_device):
     """Configs 32-35 (one workgroup per CU slot walking its blocks, next block's first chunk loaded
-    under the current epilogue) against their one-block-per-workgroup forms 28-31: same k order and
-    rounding per block, so the outputs are bit-identical, and repeated launches agree."""
+    under the current epilogue) and 38-41 (the round-5 block loop around the same block code)
+    against their one-block-per-workgroup forms 28-31: same k order and rounding per block, so the
+    outputs are bit-identical, and repeated launches agree."""
     n, cin, h, w, cout, up, pad, pool = case
     x = torch.from_numpy(synth.image(700 + cin, (n, cin, h, w)) * 2 - 0.5).to(hip_device)
     wt = torch.from_numpy(synth.conv_weight(710 + cin, cout, cin, 3)).to(hip_device)
@@ -121,13 +122,13 @@ def test_conv3x3_persistent_bit_identical(case, hip_device):
     for cfg in (28, 29, 30, 31):
         ref = ops.conv3x3(x, wp, bd, cout, upsample=up, pad_mode=pad, want_pre=True, want_act=True, want_pool=pool,
                           cfg=cfg)
-        for _ in range(2):
+        for pc in (cfg + 4, cfg + 4, cfg + 10, cfg + 10):
             got = ops.conv3x3(x, wp, bd, cout, upsample=up, pad_mode=pad, want_pre=True, want_act=True,
-                              want_pool=pool, cfg=cfg + 4)
+                              want_pool=pool, cfg=pc)
             torch.cuda.synchronize()
             for r, g in zip(ref, got):
                 if r is not None:
-                    assert torch.equal(r, g), (cfg + 4, (r - g).abs().max().item())
+                    assert torch.equal(r, g), (pc, (r - g).abs().max().item())
 
 
 @pytest.mark.parametrize("cin", [1, 2, 3, 4])
