@@ -32,10 +32,20 @@ def _f32(t, name):
     return t.contiguous()
 
 
+_AUTOSPLIT = os.environ.get("AST_MBGEMM_AUTOSPLIT", "1") != "0"
+
+
 def gemm(A, B, C, M, N, K, batch, sA, sB, sC, ksplit=1, accumulate=False, fold_k=0, fold_n=0, role=""):
     """C[b][m][n] (+)= sum_k A[b][m][k] B[b][k][n]; sA/sB/sC = (batch, row, col) element strides.
     fold_n / fold_k = P: the image index is folded into N / K (batch 1; see ast_hip.h). K-split or
-    batch-shared C tiles meet in a workspace and are summed in a fixed order (deterministic)."""
+    batch-shared C tiles meet in a workspace and are summed in a fixed order (deterministic).
+    A product with fewer than 256 64x64 tiles (the AST bottleneck's 1x1 convs at 20x20: 26-100
+    workgroups on 256 CUs) and K >= 128 is split along K to ~512 workgroups, chunks >= 64 deep
+    (AST_MBGEMM_AUTOSPLIT=0: off, for A/B runs)."""
+    if _AUTOSPLIT and ksplit == 1 and not fold_k:
+        tiles = -(-M // 64) * -(-N // 64) * batch
+        if tiles < 256 and K >= 128:
+            ksplit = max(1, min(-(-512 // tiles), K // 64))
     nws = int(lib().ast_mbt_gemm_workspace_floats(M, N, batch, ksplit, sC[0]))
     ws = workspace(nws, C.device) if nws > 0 else None
     check(ops._timed(f"mbgemm {role} {M}x{N}x{K}", 2 * M * N * K * batch, C.device, lambda: lib().ast_mbt_gemm_f32(
