@@ -112,21 +112,18 @@ def _conv_backward(ctx, g_pre, g_act, g_pool):
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[3]):
             xin = Fn.normalize_image(x, mean, std) if mean is not None else x
             dw, db = Fn.conv_weight_grad(xin, dy, cout, with_bias=has_bias)
-    else:               # the decoder walk (DecoderConvFn): padded masked gradient, dgrad, adjoint, wgrad
+    else:               # the decoder walk (DecoderConvFn.backward): ReLU mask, input grad + border fold, wgrad
         g = nz(g_act) if want_act else nz(g_pre)
         g = g.contiguous()
-        pitch = (W + 2 + 3) // 4 * 4
-        dyp = torch.empty((n, cout, H + 2, pitch), device=g.device, dtype=torch.float32)
-        check(lib().ast_grad_pad_f32(ptr(g), ptr(mask) if want_act else None, ptr(dyp), n * cout, H, W, pitch,
-                                     stream_ptr(g.device)), "grad_pad")
+        if want_act:
+            dy = torch.empty_like(g)
+            check(lib().ast_relu_mask_f32(ptr(g), ptr(mask), ptr(dy), g.numel(), stream_ptr(g.device)), "relu_mask")
+        else:
+            dy = g
         if ctx.needs_input_grad[0]:
-            dp = Fn.conv_input_grad_same(dyp, weight)
-            dx = torch.empty_like(x)
-            check(lib().ast_pad_up_adjoint_f32(ptr(dp), ptr(dx), n * cin, hin, win, upsample, pitch,
-                                               stream_ptr(g.device)), "pad_up_adjoint")
+            dx = Fn.conv_input_grad(dy, weight, upsample, "reflect")
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[3]):
-            dw, db = Fn.conv_weight_grad(x, dyp, cout, upsample, "reflect", has_bias,
-                                         dy_layout=(pitch, (H + 2) * pitch, pitch + 1))
+            dw, db = Fn.conv_weight_grad(x, dy, cout, upsample, "reflect", has_bias)
     return dx, dw, None, db, None, None, None, None, None, None, None, None
 
 

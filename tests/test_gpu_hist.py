@@ -62,11 +62,14 @@ def test_hist_loss_vs_oracle(shape):
 
 
 def test_earth_movers_module_and_pixel_mse():
+    torch.manual_seed(7)
     hx = torch.rand(3, 256)
     hy = torch.rand(3, 256)
     ref = R.earth_movers(hx, hy)
     got = L.earth_movers(hx.cuda(), hy.cuda())
-    assert rel_inf(got, ref) <= 1e-5
+    # a sum of squared 256-term cumulative sums (values ~1e3-1e4) in fp32 on both sides, in
+    # different orders: ~256 ulp of drift, so 3e-5 (unseeded inputs once landed at 1.04e-5)
+    assert rel_inf(got, ref) <= 3e-5
     a = torch.rand(2, 3, 19, 23, device="cuda", requires_grad=True)
     b = torch.rand(2, 3, 19, 23, device="cuda")
     m = L.pixel_mse_loss(a, b, 100.0)
