@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <algorithm>
 #include "../../include/ast_hip.h"
 
 namespace {
@@ -168,6 +170,8 @@ struct AttnArgs {
   const float* stats;
   void* out;  // [n][C][Nq]
   int n, C, Cp, nq, nk, nqp, nkp, qtiles;
+  int ksplit, kchunk;  // split-K over the keys, as AttnB16Args
+  float* part;
 };
 
 constexpr int BK = 32;        // keys per block
@@ -243,7 +247,8 @@ __global__ __launch_bounds__(256, 1) void attend_f32_kernel(AttnArgs a) {
   __shared__ float ks[2][CP * KP];
   __shared__ float vs[2][CP * VP];
   int b, tile;
-  map_tile(blockIdx.x, gridDim.x, a.qtiles, b, tile);
+  const int ntq = a.n * a.qtiles, sp = (int)blockIdx.x / ntq;  // split index (0 without a split)
+  map_tile((int)blockIdx.x - sp * ntq, ntq, a.qtiles, b, tile);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
   const int q0 = tile * 128;
   const int qi = q0 + wv * 32 + r;  // this lane's query (column of every accumulator tile)
@@ -271,12 +276,12 @@ __global__ __launch_bounds__(256, 1) void attend_f32_kernel(AttnArgs a) {
   }
   float mrow = -INFINITY, lsum = 0.f;  // mrow in log2 units
 
-  const int nblk = a.nkp / BK;
-  kv.load(kb, vb, tid, a.nkp, 0);
+  const int j0 = sp * a.kchunk, nblk = min(a.nkp / BK, j0 + a.kchunk);
+  kv.load(kb, vb, tid, a.nkp, j0 * BK);
   kv.template store<KP, VP>(ks[0], vs[0], tid);
   const float* qq = &qs[h * 128 + ((wv * 32 + r) ^ (h << 5))];
-  for (int j = 0; j < nblk; ++j) {
-    const int buf = j & 1;
+  for (int j = j0; j < nblk; ++j) {
+    const int buf = (j - j0) & 1;
     if (j + 1 < nblk) kv.load(kb, vb, tid, a.nkp, (j + 1) * BK);
     __syncthreads();
 
@@ -343,9 +348,28 @@ __global__ __launch_bounds__(256, 1) void attend_f32_kernel(AttnArgs a) {
     if (j + 1 < nblk) kv.template store<KP, VP>(ks[buf ^ 1], vs[buf ^ 1], tid);
   }
 
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  if (a.part) {  // this split's partials (layout of AttnB16Args::part)
+    const int64_t mq = (int64_t)a.ksplit * a.n * a.nqp;
+    float* pm = a.part + ((int64_t)sp * a.n + b) * a.nqp;
+    float* po = a.part + 2 * mq + ((int64_t)sp * a.n + b) * 2 * CP * a.nqp;
+    if (h == 0) {
+      pm[qi] = mrow;
+      pm[mq + qi] = ltot;
+    }
+#pragma unroll
+    for (int t = 0; t < CT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ch = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        po[(int64_t)ch * a.nqp + qi] = om[t][i];
+        po[(int64_t)(CP + ch) * a.nqp + qi] = osq[t][i];
+      }
+    return;
+  }
   // Epilogue: out[b][ch][qi] = std * (c - mean_c) * rstd_c + mean.
   if (qi >= a.nq) return;
-  const float inv = 1.0f / (lsum + __shfl_xor(lsum, 32, 64));
+  const float inv = 1.0f / ltot;
   const float* cmean = a.stats + (int64_t)b * a.C;
   const float* crstd = a.stats + (int64_t)a.n * a.C + (int64_t)b * a.C;
   const TO* __restrict__ cb = (const TO*)a.c + (int64_t)b * a.C * a.nq;
@@ -510,6 +534,11 @@ struct AttnB16Args {
   const float* vmean;  // [n][C]
   bf16* out;
   int n, C, Cp, nq, nk, nqp, nkp, qtiles;
+  // split-K over the keys (flash-decoding; small batches): split s of ksplit takes key blocks
+  // [s kchunk, (s + 1) kchunk) and writes its running max, sum and unnormalised [V, V^2] sums to
+  // part ([ksplit][n][nqp] m, then l, then [ksplit][n][2 Cp][nqp]); attn_merge_kernel combines them
+  int ksplit, kchunk;
+  float* part;
 };
 
 // 8 waves x 32 queries per workgroup, 32-key blocks, v_mfma_f32_32x32x16_bf16.
@@ -530,7 +559,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attend_bf16_kernel(AttnB16Arg
   __shared__ __attribute__((aligned(16))) bf16 vs[2][CP * VPB];
   __shared__ __attribute__((aligned(16))) bf16 v2s[2][CP * VPB];
   int b, tile;
-  map_tile(blockIdx.x, gridDim.x, a.qtiles, b, tile);
+  const int ntq = a.n * a.qtiles, sp = (int)blockIdx.x / ntq;  // split index (0 without a split)
+  map_tile((int)blockIdx.x - sp * ntq, ntq, a.qtiles, b, tile);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
   const int qi = tile * (NW * 32) + wv * 32 + r;
 
@@ -593,11 +623,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attend_bf16_kernel(AttnB16Arg
   }
   float mrow = -INFINITY;
   f32x2 lsum2 = {0.f, 0.f};
-  const int nblk = a.nkp / BK;
-  gload(0);
+  const int j0 = sp * a.kchunk, nblk = min(a.nkp / BK, j0 + a.kchunk);
+  gload(j0 * BK);
   lstore(0);
-  for (int j = 0; j < nblk; ++j) {
-    const int buf = j & 1;
+  for (int j = j0; j < nblk; ++j) {
+    const int buf = (j - j0) & 1;
     if (j + 1 < nblk) gload((j + 1) * BK);
     __syncthreads();
 
@@ -662,9 +692,28 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attend_bf16_kernel(AttnB16Arg
     if (j + 1 < nblk) lstore(buf ^ 1);
   }
 
-  if (qi >= a.nq) return;
   const float lsum = lsum2[0] + lsum2[1];
-  const float inv = 1.0f / (lsum + __shfl_xor(lsum, 32, 64));
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  if (a.part) {  // this split's partials (all nqp queries; the merge reads the first nq)
+    const int64_t mq = (int64_t)a.ksplit * a.n * a.nqp;
+    float* pm = a.part + ((int64_t)sp * a.n + b) * a.nqp;
+    float* po = a.part + 2 * mq + ((int64_t)sp * a.n + b) * 2 * CP * a.nqp;
+    if (h == 0) {
+      pm[qi] = mrow;
+      pm[mq + qi] = ltot;
+    }
+#pragma unroll
+    for (int t = 0; t < CT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ch = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        po[(int64_t)ch * a.nqp + qi] = om[t][i];
+        po[(int64_t)(CP + ch) * a.nqp + qi] = osq[t][i];
+      }
+    return;
+  }
+  if (qi >= a.nq) return;
+  const float inv = 1.0f / ltot;
   const float* cmean = a.stats + (int64_t)b * a.C;
   const float* crstd = a.stats + (int64_t)a.n * a.C + (int64_t)b * a.C;
   const float* vm = a.vmean + (int64_t)b * a.C;
@@ -686,6 +735,47 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attend_bf16_kernel(AttnB16Arg
     }
 }
 
+// The splits of attend_*_kernel combined, in split order, then the epilogue: with M = max_s m_s,
+// w_s = 2^(m_s - M): mean = sum w_s O_s / sum w_s l_s, E[v^2] likewise (bf16: + the V mean).
+struct MergeArgs {
+  const void* c;
+  const float* stats;
+  const float* vmean;  // null on the fp32 path (V not centred)
+  void* out;
+  const float* part;
+  int n, C, Cp, nq, nqp, ksplit;
+};
+
+template <typename TO>
+__global__ __launch_bounds__(256) void attn_merge_kernel(MergeArgs a) {
+  const int64_t total = (int64_t)a.n * a.C * a.nq;
+  const int64_t mq = (int64_t)a.ksplit * a.n * a.nqp;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int q = (int)(idx % a.nq);
+    const int64_t bc = idx / a.nq;
+    const int ch = (int)(bc % a.C), b = (int)(bc / a.C);
+    float M = -INFINITY;
+    for (int s = 0; s < a.ksplit; ++s) M = fmaxf(M, a.part[((int64_t)s * a.n + b) * a.nqp + q]);
+    float L = 0.f, O = 0.f, O2 = 0.f;
+    for (int s = 0; s < a.ksplit; ++s) {
+      const int64_t mi = ((int64_t)s * a.n + b) * a.nqp + q;
+      const float w = __builtin_amdgcn_exp2f(a.part[mi] - M);
+      const float* po = a.part + 2 * mq + ((int64_t)s * a.n + b) * 2 * a.Cp * a.nqp;
+      L = fmaf(w, a.part[mq + mi], L);
+      O = fmaf(w, po[(int64_t)ch * a.nqp + q], O);
+      O2 = fmaf(w, po[(int64_t)(a.Cp + ch) * a.nqp + q], O2);
+    }
+    const float inv = 1.0f / L;
+    const float mean = O * inv;
+    float var = fmaf(-mean, mean, O2 * inv);
+    var = var < 0.f ? 0.f : var;
+    const int64_t o = ((int64_t)b * a.C + ch) * a.nq + q;
+    const float xn = ((float)((const TO*)a.c)[o] - a.stats[(int64_t)b * a.C + ch]) *
+                     a.stats[(int64_t)a.n * a.C + (int64_t)b * a.C + ch];
+    ((TO*)a.out)[o] = (TO)fmaf(sqrtf(var), xn, a.vmean ? mean + a.vmean[(int64_t)b * a.C + ch] : mean);
+  }
+}
+
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
 }  // namespace
@@ -694,9 +784,25 @@ inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 namespace {
 
 struct AttnLayout {  // workspace carve-up (bytes), shared by the size query and the launcher
-  int cp, nqp, nkp;
-  size_t stats, vmean, q, k, v, v2, total;
+  int cp, nqp, nkp, ksplit, kchunk;
+  size_t stats, vmean, q, k, v, v2, part, total;
 };
+
+// bf16 path: split the keys when the query tiles leave the chip underfilled (< 256 workgroups):
+// ~512 workgroups, >= 2 key blocks per split (AST_ATTN_KSPLIT=0: never, for A/B runs)
+void attn_split(int dtype, int n, int nqp, int nkp, int& ksplit, int& kchunk) {
+  static const int on = [] {
+    const char* v = getenv("AST_ATTN_KSPLIT");
+    return v ? atoi(v) : 1;
+  }();
+  const int nblk = nkp / BK;
+  const bool big = dtype != 0 && (int64_t)n * (nqp / 256) >= 512;  // fp32: 128 queries per workgroup
+  const int64_t wgs = (int64_t)n * (nqp / (big ? 256 : 128));
+  int ks = 1;
+  if (on && wgs < 256 && nblk >= 4) ks = (int)std::min<int64_t>((512 + wgs - 1) / wgs, nblk / 2);
+  kchunk = (nblk + ks - 1) / ks;
+  ksplit = (nblk + kchunk - 1) / kchunk;  // every split non-empty
+}
 
 AttnLayout attn_layout(int dtype, int n, int c, int nq, int nk) {
   AttnLayout L;
@@ -711,7 +817,9 @@ AttnLayout attn_layout(int dtype, int n, int c, int nq, int nk) {
   L.k = L.q + al(es * (size_t)n * L.cp * L.nqp);
   L.v = L.k + al(es * (size_t)n * L.cp * L.nkp);
   L.v2 = L.v + al(es * (size_t)n * L.cp * L.nkp);
-  L.total = L.v2 + (dtype == 0 ? 0 : al(es * (size_t)n * L.cp * L.nkp));
+  L.part = dtype == 0 ? L.v2 : L.v2 + al(es * (size_t)n * L.cp * L.nkp);
+  attn_split(dtype, n, L.nqp, L.nkp, L.ksplit, L.kchunk);
+  L.total = L.part + (L.ksplit > 1 ? al(sizeof(float) * (size_t)L.ksplit * n * L.nqp * (2 + 2 * (size_t)L.cp)) : 0);
   return L;
 }
 
@@ -760,10 +868,18 @@ int ast_adaattn_fwd(int dtype, const void* content, const void* style, const flo
     if ((e = set_lds(proj, plds)) != hipSuccess) return (int)e;
     hipLaunchKernelGGL(proj, pgrid, dim3(256), plds, st, pa);
     const int qtiles = nqp / 128;
-    AttnArgs aa{q, k, v, content, stats, out, n, c, cp, nq, nk, nqp, nkp, qtiles};
+    float* part = L.ksplit > 1 ? (float*)(wsb + L.part) : nullptr;
+    AttnArgs aa{q, k, v, content, stats, out, n, c, cp, nq, nk, nqp, nkp, qtiles, L.ksplit, L.kchunk, part};
     void (*att)(AttnArgs) = ct == 1 ? attend_f32_kernel<float, 1> : ct == 2 ? attend_f32_kernel<float, 2>
                           : ct == 3 ? attend_f32_kernel<float, 3> : attend_f32_kernel<float, 4>;
-    hipLaunchKernelGGL(att, dim3((unsigned)(n * qtiles)), dim3(256), 0, st, aa);
+    hipLaunchKernelGGL(att, dim3((unsigned)(n * qtiles * L.ksplit)), dim3(256), 0, st, aa);
+    if (L.ksplit > 1) {
+      if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+      const int64_t tot = (int64_t)n * c * nq;
+      MergeArgs ma{content, stats, nullptr, out, part, n, c, cp, nq, nqp, L.ksplit};
+      hipLaunchKernelGGL(attn_merge_kernel<float>, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, 8192)), dim3(256),
+                         0, st, ma);
+    }
     return (int)hipGetLastError();
   }
 
@@ -785,7 +901,9 @@ int ast_adaattn_fwd(int dtype, const void* content, const void* style, const flo
   // problems (< 512 such workgroups) use 4-wave workgroups instead, to spread over more CUs.
   const bool big = (int64_t)n * (nqp / 256) >= 512;
   const int nw = big ? 8 : 4, qtiles = nqp / (nw * 32);
-  AttnB16Args aa{q, k, v, v2, (const bf16*)content, stats, vmean, (bf16*)out, n, c, cp, nq, nk, nqp, nkp, qtiles};
+  float* part = L.ksplit > 1 ? (float*)(wsb + L.part) : nullptr;
+  AttnB16Args aa{q, k, v, v2, (const bf16*)content, stats, vmean, (bf16*)out, n, c, cp, nq, nk, nqp, nkp, qtiles,
+                 L.ksplit, L.kchunk, part};
   void (*att)(AttnB16Args);
   if (big)
     att = ct == 1 ? attend_bf16_kernel<1, 8> : ct == 2 ? attend_bf16_kernel<2, 8> : ct == 3 ? attend_bf16_kernel<3, 8>
@@ -793,7 +911,14 @@ int ast_adaattn_fwd(int dtype, const void* content, const void* style, const flo
   else
     att = ct == 1 ? attend_bf16_kernel<1, 4> : ct == 2 ? attend_bf16_kernel<2, 4> : ct == 3 ? attend_bf16_kernel<3, 4>
                                                                                     : attend_bf16_kernel<4, 4>;
-  hipLaunchKernelGGL(att, dim3((unsigned)(n * qtiles)), dim3(nw * 64), 0, st, aa);
+  hipLaunchKernelGGL(att, dim3((unsigned)(n * qtiles * L.ksplit)), dim3(nw * 64), 0, st, aa);
+  if (L.ksplit > 1) {
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    const int64_t tot = (int64_t)n * c * nq;
+    MergeArgs ma{content, stats, vmean, out, part, n, c, cp, nq, nqp, L.ksplit};
+    hipLaunchKernelGGL(attn_merge_kernel<bf16>, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, 8192)), dim3(256),
+                       0, st, ma);
+  }
   return (int)hipGetLastError();
 }
 

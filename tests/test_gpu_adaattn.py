@@ -62,6 +62,7 @@ def _case(seed, n, c, hc, wc, hs, ws, qk_scale):
     (1, 128, 40, 40, 33, 31),  # Nq = 1600 (13 query tiles), Nk = 1023
     (2, 8, 17, 3, 2, 40),      # C = 8 (one padded channel tile), tall/wide maps
     (1, 100, 12, 12, 16, 16),  # C not a multiple of 32 or 8
+    (1, 128, 64, 64, 64, 64),  # n = 1 at 64^2: keys split 8 ways, merged in split order
 ])
 def test_adaattn_vs_oracle(shape):
     n, c, hc, wc, hs, ws = shape
@@ -124,6 +125,43 @@ def test_adaattn_bf16_vs_oracle(shape):
     torch.cuda.synchronize()
     assert out.dtype == torch.bfloat16
     assert rel_inf(out.float(), ref) <= 2e-2, (shape, rel_inf(out.float(), ref))
+
+
+@pytest.mark.parametrize("shape", [
+    (1, 128, 64, 64, 64, 64),   # n = 1 at 64^2: 32 query tiles, keys split 8 ways (flash-decoding)
+    (1, 64, 48, 40, 33, 35),    # ragged keys (Nk = 1155), uneven last split
+])
+def test_adaattn_bf16_split_keys(shape):
+    """Small batches split the keys (attn_split, csrc/adaattn.hip) and merge the splits' partial
+    softmax statistics in split order: against the oracle at the bf16 bar, against the unsplit
+    kernel (a child process with AST_ATTN_KSPLIT=0) within fp32 reordering of the bf16 P V sums,
+    and repeatable bit for bit."""
+    import os
+    import subprocess
+    import sys
+    n, c, hc, wc, hs, ws = shape
+    x, y, w = _case(3000 + c, n, c, hc, wc, hs, ws, 0.15)
+    xb, yb = _bf16_round(x), _bf16_round(y)
+    args = (xb.to(torch.bfloat16).cuda(), yb.to(torch.bfloat16).cuda(), *(T(t) for t in w))
+    out = ops.adaattn(*args)
+    again = ops.adaattn(*args)
+    ref = R.adaattn(xb, yb, *(torch.from_numpy(t) for t in w))
+    torch.cuda.synchronize()
+    assert torch.equal(out, again)
+    assert rel_inf(out.float(), ref) <= 2e-2, rel_inf(out.float(), ref)
+    code = ("import sys, torch, numpy as np; sys.path.insert(0, '.'); from arbitrarystyletransfer_amd import ops; "
+            "d = np.load(sys.argv[1]); T = lambda a: torch.from_numpy(a).cuda(); "
+            "o = ops.adaattn(T(d['x']).to(torch.bfloat16), T(d['y']).to(torch.bfloat16), T(d['wq']), T(d['wk']), "
+            "T(d['wv'])); np.save(sys.argv[2], o.float().cpu().numpy())")
+    import tempfile
+    with tempfile.TemporaryDirectory() as tmp:
+        src, dst = os.path.join(tmp, "in.npz"), os.path.join(tmp, "out.npy")
+        np.savez(src, x=xb.numpy(), y=yb.numpy(), wq=w[0], wk=w[1], wv=w[2])
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        subprocess.run([sys.executable, "-c", code, src, dst], cwd=root, check=True, timeout=240,
+                       env=dict(os.environ, AST_ATTN_KSPLIT="0"))
+        unsplit = torch.from_numpy(np.load(dst))
+    assert rel_inf(out.float(), unsplit) <= 1e-2, rel_inf(out.float(), unsplit)
 
 
 @pytest.mark.parametrize("regime", ["diffuse", "live"])
