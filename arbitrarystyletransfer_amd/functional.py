@@ -211,12 +211,16 @@ class LossNetFn(torch.autograd.Function):
         plan = net._plan()
         outs, pres, ins = [], [], []
         cur = x
-        for idx, conv, want_pre, want_act, want_pool, collect in plan:
+        for k, (idx, conv, want_pre, want_act, want_pool, collect) in enumerate(plan):
             first = idx == 1
+            # the pre-ReLU map is kept only where the backward reads it: under a max-pool (argmax
+            # routing) and at the top layer; elsewhere the next conv's input (the ReLU output) is the
+            # mask, so a layer without a conv_i tap stores its ReLU output alone
+            keep_pre = want_pre or want_pool or k == len(plan) - 1
             pre, act, pool = ops.conv3x3(cur, net._packed.get(conv), conv.bias, conv.out_channels, pad_mode="zeros",
                                          in_mean=norm.mean.view(-1) if first else None,
                                          in_std=norm.std.view(-1) if first else None,
-                                         want_pre=True, want_act=want_act, want_pool=want_pool)
+                                         want_pre=keep_pre, want_act=want_act, want_pool=want_pool)
             by_name = {conv.name: pre, f"relu_{idx}": act, f"pool_{idx}": pool}
             outs.extend(by_name[nm] for nm in collect)
             pres.append(pre)
@@ -246,7 +250,9 @@ class LossNetFn(torch.autograd.Function):
                 gq = g_pool if gq is None else gq + g_pool
             if gp is None and ga is None and gq is None:
                 return None
-            pre = pres[j]
+            # act > 0 exactly where pre > 0: a layer without a stored pre-ReLU map (no pool below it)
+            # masks by its ReLU output, the next conv's input
+            pre = pres[j] if pres[j] is not None else ins[j + 1]
             n, c, h, w = pre.shape
             dy = torch.empty_like(pre)
             check(lib().ast_conv_act_backward_f32(ptr(pre), ptr(_dev(gp, "g") if gp is not None else None),
