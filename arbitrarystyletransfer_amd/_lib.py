@@ -42,7 +42,7 @@ SIGNATURES = {
     "ast_pad_up_adjoint_f32": (_i, [_p, _p, _ll, _i, _i, _i, _i, _p]),
     "ast_conv3x3_dgrad_f32": (_i, [_i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
     "ast_dgrad_finish_f32": (_i, [_p, _p, _p, _p, _p, _ll, _i, _i, _i, _p]),
-    "ast_dgrad_reflect_border_workspace_floats": (_ll, [_i, _i, _i, _i, _i]),
+    "ast_dgrad_reflect_border_workspace_floats": (_ll, [_i, _i, _i, _i, _i, _i]),
     "ast_dgrad_reflect_border_f32": (_i, [_p, _p, _p, _p, _p, _ll, _i, _i, _i, _i, _i, _i, _p]),
     "ast_conv3x3_wgrad_workspace_floats": (_ll, [_i, _i, _i, _i, _i, _i]),
     "ast_conv3x3_wgrad_f32": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _ll, _p]),

@@ -343,9 +343,24 @@ __global__ void dgrad_finish_kernel(const float* __restrict__ raw, float* __rest
 // per element, no atomics.
 constexpr int BL_CI = 32, BL_Q = 64, BL_CO = 32;
 
-__global__ __launch_bounds__(256) void border_lines_kernel(const float* __restrict__ dy, const float* __restrict__ wt,
-                                                           float* __restrict__ lines, int cout, int cin, int H, int W,
-                                                           int Lp) {
+// dy's first and last columns made contiguous, cols[n][cout][2][H] (one strided pass; the line
+// kernel's column lines then read them like its row lines, instead of re-reading one 4-byte word
+// per 64-byte line from every ci block)
+__global__ __launch_bounds__(256) void border_cols_kernel(const float* __restrict__ dy, float* __restrict__ cols,
+                                                          int64_t rows, int H, int W) {
+  // rows = n * cout * 2 * H: (plane, side, y)
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < rows; i += (int64_t)gridDim.x * 256) {
+    const int y = (int)(i % H);
+    const int64_t ps = i / H;
+    const int side = (int)(ps & 1);
+    const int64_t pl = ps >> 1;
+    cols[i] = dy[(pl * H + y) * W + (side ? W - 1 : 0)];
+  }
+}
+
+__global__ __launch_bounds__(256) void border_lines_kernel(const float* __restrict__ dy, const float* __restrict__ cols,
+                                                           const float* __restrict__ wt, float* __restrict__ lines,
+                                                           int cout, int cin, int H, int W, int Lp) {
   __shared__ float Ds[BL_CO][BL_Q + 2];
   __shared__ float Ws[BL_CO][BL_CI][3];
   const int line = blockIdx.z & 3, n = blockIdx.z >> 2;
@@ -353,12 +368,11 @@ __global__ __launch_bounds__(256) void border_lines_kernel(const float* __restri
   const bool row = line < 2;
   const int L = row ? W : H;
   if (q0 >= L + 2) return;
-  const int64_t plane = (int64_t)H * W;
-  // line start and element stride in a dy plane; the fixed tap of the other axis
-  const int64_t base = row ? (line == 0 ? 0 : (int64_t)(H - 1) * W) : (line == 2 ? 0 : W - 1);
-  const int stride = row ? 1 : W;
+  // a line's source per output channel: a dy row (rows), or a contiguous column of cols
+  const int64_t plane = row ? (int64_t)H * W : 2 * (int64_t)H;
   const int fixed = (line & 1) ? 2 : 0;
-  const float* dyn = dy + (int64_t)n * cout * plane + base;
+  const float* dyn = row ? dy + (int64_t)n * cout * plane + (line == 0 ? 0 : (int64_t)(H - 1) * W)
+                         : cols + (int64_t)n * cout * plane + (line == 2 ? 0 : H);
   const int t = threadIdx.x, ci = t >> 3, qg = t & 7;
   float acc[8];
 #pragma unroll
@@ -367,7 +381,7 @@ __global__ __launch_bounds__(256) void border_lines_kernel(const float* __restri
     __syncthreads();
     for (int e = t; e < BL_CO * (BL_Q + 2); e += 256) {
       const int co = e / (BL_Q + 2), j = e - co * (BL_Q + 2), src = q0 - 2 + j;
-      Ds[co][j] = (c0 + co < cout && src >= 0 && src < L) ? dyn[(int64_t)(c0 + co) * plane + (int64_t)src * stride] : 0.f;
+      Ds[co][j] = (c0 + co < cout && src >= 0 && src < L) ? dyn[(int64_t)(c0 + co) * plane + src] : 0.f;
     }
     for (int e = t; e < BL_CO * BL_CI * 3; e += 256) {
       const int co = e / (BL_CI * 3), r = e - co * (BL_CI * 3), cc = r / 3, k = r - 3 * cc;
@@ -1130,9 +1144,10 @@ int ast_dgrad_finish_f32(const float* raw, float* dx, const float* mask, const f
   return (int)hipGetLastError();
 }
 
-long long ast_dgrad_reflect_border_workspace_floats(int n, int cin, int h, int w_in, int upsample) {
-  if (n <= 0 || cin <= 0 || h <= 0 || w_in <= 0 || (upsample != 1 && upsample != 2)) return 0;
-  return (long long)n * 4 * cin * (std::max(h, w_in) * upsample + 2);
+long long ast_dgrad_reflect_border_workspace_floats(int n, int cout, int cin, int h, int w_in, int upsample) {
+  if (n <= 0 || cout <= 0 || cin <= 0 || h <= 0 || w_in <= 0 || (upsample != 1 && upsample != 2)) return 0;
+  // the four lines [n][4][cin][max(H, W) + 2], then dy's edge columns [n][cout][2][H]
+  return (long long)n * 4 * cin * (std::max(h, w_in) * upsample + 2) + (long long)n * cout * 2 * h * upsample;
 }
 
 int ast_dgrad_reflect_border_f32(const float* dy, const float* w, float* dx, const float* mask, float* workspace,
@@ -1144,11 +1159,17 @@ int ast_dgrad_reflect_border_f32(const float* dy, const float* w, float* dx, con
   if (h * upsample < 2 || w_in * upsample < 2) return AST_E_SHAPE;  // ReflectionPad2d(1) needs size >= 2
   if ((int64_t)n * cin >= 65536 || (int64_t)n * 4 >= 65536 || (int64_t)cout * h * w_in * upsample * upsample >= ((int64_t)1 << 31))
     return AST_E_SHAPE;
-  if (workspace_floats < ast_dgrad_reflect_border_workspace_floats(n, cin, h, w_in, upsample)) return AST_E_SHAPE;
+  if (workspace_floats < ast_dgrad_reflect_border_workspace_floats(n, cout, cin, h, w_in, upsample)) return AST_E_SHAPE;
   const int H = h * upsample, W = w_in * upsample, Lp = std::max(H, W) + 2;
-  hipLaunchKernelGGL(border_lines_kernel, dim3((Lp + BL_Q - 1) / BL_Q, (cin + BL_CI - 1) / BL_CI, n * 4), dim3(256), 0,
-                     (hipStream_t)stream, dy, w, workspace, cout, cin, H, W, Lp);
+  float* cols = workspace + (int64_t)n * 4 * cin * Lp;
+  const int64_t crows = (int64_t)n * cout * 2 * H;
+  hipLaunchKernelGGL(border_cols_kernel, dim3((unsigned)std::min<int64_t>((crows + 255) / 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, dy, cols, crows, H, W);
   int e = (int)hipGetLastError();
+  if (e) return e;
+  hipLaunchKernelGGL(border_lines_kernel, dim3((Lp + BL_Q - 1) / BL_Q, (cin + BL_CI - 1) / BL_CI, n * 4), dim3(256), 0,
+                     (hipStream_t)stream, dy, cols, w, workspace, cout, cin, H, W, Lp);
+  e = (int)hipGetLastError();
   if (e) return e;
   const int rt = 1 / upsample, rb = (H - 2) / upsample, ct = 1 / upsample, cr = (W - 2) / upsample;
   const int nrow = rb != rt ? 2 : 1, ncol = cr != ct ? 2 : 1;

@@ -106,7 +106,7 @@ def conv_input_grad(dy, weight, upsample=1, pad_mode="zeros", in_scale=None, mas
             check(code, "conv3x3_dgrad")
     if pad_mode == "reflect":
         wt = _dev(weight.detach(), "weight")
-        ws = workspace(lib().ast_dgrad_reflect_border_workspace_floats(n, cin, h, w, up), dy.device)
+        ws = workspace(lib().ast_dgrad_reflect_border_workspace_floats(n, cout, cin, h, w, up), dy.device)
         check(lib().ast_dgrad_reflect_border_f32(ptr(dy), ptr(wt), ptr(dx), ptr(mask), ptr(ws), ws.numel(), n, cout,
                                                  cin, h, w, up, _s(dy)), "dgrad_reflect_border")
     return dx

@@ -184,10 +184,11 @@ int ast_dgrad_finish_f32(const float* raw, float* dx, const float* mask, const f
 
 /* Reflect-pad border of the input gradient of conv3x3(ReflectionPad2d(1)(upsample(x))): adds to
  * dx [n, cin, h, w_in] the padded-input gradient's four border lines (computed from dy [n, cout,
- * h*up, w_in*up] and the forward filter w [cout, cin, 3, 3] into the workspace) folded as the
+ * h*up, w_in*up] and the forward filter w [cout, cin, 3, 3] into the workspace, with dy's edge
+ * columns made contiguous there first) folded as the
  * reflect pad and upsample map them, masked like the interior (mask [n, cin, h, w_in] > 0, or
  * NULL). workspace: ast_dgrad_reflect_border_workspace_floats floats. */
-long long ast_dgrad_reflect_border_workspace_floats(int n, int cin, int h, int w_in, int upsample);
+long long ast_dgrad_reflect_border_workspace_floats(int n, int cout, int cin, int h, int w_in, int upsample);
 int ast_dgrad_reflect_border_f32(const float* dy, const float* w, float* dx, const float* mask,
                                  float* workspace, long long workspace_floats, int n, int cout,
                                  int cin, int h, int w_in, int upsample, void* stream);
