@@ -646,7 +646,21 @@ __global__ __launch_bounds__(256) void wgrad_smallco_kernel(WgArgs a) {
   }
   const int64_t t0 = a.tiles_per_block * split;
   const int64_t t1 = min(a.ntiles, t0 + a.tiles_per_block);
-  for (int64_t tile = t0; tile < t1; ++tile) {
+  // register prefetch (round 5): the next tile's input halo and dY are loaded while this tile's
+  // FMAs run (the staging was latency-bound: loads -> barrier -> dY loads -> FMAs per tile).
+  // Per-thread staging coordinates are fixed across tiles; same products in the same order.
+  constexpr int NX = (SC_CG * SC_PS + 255) / 256;
+  int xc[NX], xr[NX], xcol[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    const int e = tid + 256 * i, rc = e % SC_PS;
+    xc[i] = e / SC_PS;
+    xr[i] = rc / SC_RS;
+    xcol[i] = rc % SC_RS;
+  }
+  float xv[NX], dv[COUT];
+  bool dok = false;
+  auto load = [&](int64_t tile) {
     int64_t tt = tile;
     const int bx = (int)(tt % a.tiles_x);
     tt /= a.tiles_x;
@@ -654,29 +668,40 @@ __global__ __launch_bounds__(256) void wgrad_smallco_kernel(WgArgs a) {
     const int n = (int)(tt / a.tiles_y);
     const int x0 = bx * SC_TW, y0 = by * SC_TH;
     const float* xin = a.x + ((int64_t)n * a.Cin + ci0) * Hin * Win;
-    __syncthreads();
-    for (int e = tid; e < SC_CG * SC_PS; e += 256) {
-      const int c = e / SC_PS, rc = e % SC_PS, r = rc / SC_RS, col = rc % SC_RS;
-      int gy = y0 - 1 + r, gx = x0 - 1 + col;   // padded, upsampled grid
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
       float v = 0.f;
-      if (ci0 + c < a.Cin) {
+      if (tid + 256 * i < SC_CG * SC_PS && ci0 + xc[i] < a.Cin) {
+        int gy = y0 - 1 + xr[i], gx = x0 - 1 + xcol[i];   // padded, upsampled grid
         bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
         if (!ok && a.reflect && gy >= -1 && gy <= H && gx >= -1 && gx <= W) {
           gy = gy < 0 ? -gy : (gy >= H ? 2 * (H - 1) - gy : gy);
           gx = gx < 0 ? -gx : (gx >= W ? 2 * (W - 1) - gx : gx);
           ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
         }
-        if (ok) v = xin[((int64_t)c * Hin + gy / UP) * Win + gx / UP];
+        if (ok) v = xin[((int64_t)xc[i] * Hin + gy / UP) * Win + gx / UP];
       }
-      xs[e] = v;
+      xv[i] = v;
     }
-    __syncthreads();
     const int yy = y0 + ty, xx = x0 + tx;
-    if (yy < H && xx < W) {
-      const float* dyn = a.dy + (int64_t)n * a.Cout * a.dy_plane + a.dy_off + (int64_t)yy * a.dy_pitch + xx;
-      float d[COUT];
+    dok = yy < H && xx < W;
+    const float* dyn = a.dy + (int64_t)n * a.Cout * a.dy_plane + a.dy_off + (int64_t)yy * a.dy_pitch + xx;
 #pragma unroll
-      for (int o = 0; o < COUT; ++o) d[o] = o < a.Cout ? dyn[(int64_t)o * a.dy_plane] : 0.f;
+    for (int o = 0; o < COUT; ++o) dv[o] = (dok && o < a.Cout) ? dyn[(int64_t)o * a.dy_plane] : 0.f;
+  };
+  if (t0 < t1) load(t0);
+  for (int64_t tile = t0; tile < t1; ++tile) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NX; ++i)
+      if (tid + 256 * i < SC_CG * SC_PS) xs[tid + 256 * i] = xv[i];
+    __syncthreads();
+    const bool cur_ok = dok;
+    float d[COUT];
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) d[o] = dv[o];
+    if (tile + 1 < t1) load(tile + 1);
+    if (cur_ok) {
 #pragma unroll
       for (int o = 0; o < COUT; ++o) bacc[o] += d[o];
 #pragma unroll
