@@ -56,9 +56,11 @@ struct GemmArgs {
   float* part;  // partial tiles [batch * ksplit][M][N], or null: C written directly
   int64_t sAb, sAm, sAk, sBb, sBk, sBn, sCb, sCm, sCn;
   int M, N, K, batch, ksplit, kchunk, accumulate, foldK, foldN;
+  int vecA, vecB;  // k-contiguous A / B read as float4 runs of 4 k (host-checked alignment, below)
 };
 
 typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4g __attribute__((ext_vector_type(4)));
 constexpr int GT = 64, GK = 32, GP = GT + 1, GL = GK * GT / kT;
 
 __global__ __launch_bounds__(kT) void gemm_kernel(GemmArgs a) {
@@ -89,8 +91,32 @@ __global__ __launch_bounds__(kT) void gemm_kernel(GemmArgs a) {
     }
   }
   f32x8 ra, rb;
+  // float4 staging of a k-contiguous operand: thread t loads k = 4 (t & 7) .. + 3 of rows t >> 3 and
+  // (t >> 3) + 32 -- two 16-byte loads where the scalar map makes eight 4-byte ones; a run of 4 k
+  // never straddles an image or the chunk end (K, kchunk, foldK multiples of 4: host-checked)
+  const int v_k = 4 * (tid & 7), v_r = tid >> 3;
+  auto vload = [&](const float* base, int64_t sRow, int64_t sImg, int r0, int rmax, int k0, int kend_) {
+    const int gk = k0 + v_k;
+    int64_t kb = gk;
+    if (a.foldK) {
+      const int bb = gk / a.foldK;
+      kb = bb * sImg + (int64_t)(gk - bb * a.foldK);
+    }
+    f32x8 v;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int gr = r0 + v_r + 32 * p;
+      const f32x4g q = (gk < kend_ && gr < rmax) ? *reinterpret_cast<const f32x4g*>(base + (int64_t)gr * sRow + kb)
+                                                 : f32x4g{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * p + j] = q[j];
+    }
+    return v;
+  };
   auto load = [&](int k0) {
-    if (akf) {
+    if (akf && a.vecA) {
+      ra = vload(A, a.sAm, a.sAb, m0, a.M, k0, kend);
+    } else if (akf) {
       const int gk = k0 + a_k;
       int64_t kb = gk;
       if (a.foldK) {
@@ -115,6 +141,8 @@ __global__ __launch_bounds__(kT) void gemm_kernel(GemmArgs a) {
         const int gk = k0 + b_k + 4 * i;
         rb[i] = (gk < kend && n0 + b_n < a.N) ? B[(int64_t)gk * a.sBk + bcol] : 0.f;
       }
+    } else if (a.vecB) {
+      rb = vload(B, a.sBn, a.sBb, n0, a.N, k0, kend);
     } else {
       const int gk = k0 + b_k2;
       int64_t kb = (int64_t)gk * a.sBk;
@@ -134,9 +162,11 @@ __global__ __launch_bounds__(kT) void gemm_kernel(GemmArgs a) {
   for (int k0 = kbeg; k0 < kend; k0 += GK) {
 #pragma unroll
     for (int i = 0; i < GL; ++i) {
-      if (akf) As[a_k * GP + a_m + 8 * i] = ra[i];
+      if (akf && a.vecA) As[(v_k + (i & 3)) * GP + v_r + 32 * (i >> 2)] = ra[i];
+      else if (akf) As[a_k * GP + a_m + 8 * i] = ra[i];
       else As[(a_k2 + 4 * i) * GP + a_m2] = ra[i];
       if (bnf) Bs[(b_k + 4 * i) * GP + b_n] = rb[i];
+      else if (a.vecB) Bs[(v_k + (i & 3)) * GP + v_r + 32 * (i >> 2)] = rb[i];
       else Bs[b_k2 * GP + b_n2 + 8 * i] = rb[i];
     }
     __syncthreads();
@@ -1078,8 +1108,17 @@ int ast_mbt_gemm_f32(const float* A, const float* B, float* C, int M, int N, int
   if (need > 0 && !workspace) return AST_E_NULLPTR;
   if (workspace_floats < need) return AST_E_SHAPE;
   GemmArgs a{A, B, C, need > 0 ? workspace : nullptr, sAb, sAm, sAk, sBb, sBk, sBn, sCb, sCm, sCn, M, N, K, batch,
-             ksplit, 0, accumulate, foldK, foldN};
+             ksplit, 0, accumulate, foldK, foldN, 0, 0};
   a.kchunk = ((K + ksplit - 1) / ksplit + GK - 1) / GK * GK;
+  {  // float4 k-runs: K, the chunk and the folded image stride multiples of 4, 16-byte aligned rows
+    static const int vec = [] {  // AST_MBGEMM_VEC=0: scalar staging (A/B runs)
+      const char* v = getenv("AST_MBGEMM_VEC");
+      return v ? atoi(v) : 1;
+    }();
+    const bool kok = vec && K % 4 == 0 && a.kchunk % 4 == 0 && (foldK == 0 || foldK % 4 == 0);
+    a.vecA = kok && sAk == 1 && sAm % 4 == 0 && sAb % 4 == 0 && ((uintptr_t)A & 15) == 0;
+    a.vecB = kok && sBk == 1 && sBn != 1 && sBn % 4 == 0 && sBb % 4 == 0 && ((uintptr_t)B & 15) == 0;
+  }
   hipStream_t st = (hipStream_t)stream;
   // AST_MBGEMM_X3=1: the split-bf16 kernel (fp32-level accuracy, repeatable; measured 3% slower
   // on the AST step than the fp32-MFMA kernel, whose skinny-K shapes are latency-, not MFMA-bound)

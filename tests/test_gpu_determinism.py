@@ -104,6 +104,54 @@ def test_mbt_gemm_ksplit_and_shared(hip_device):
     twice(shared)
 
 
+_GEMM_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, '.')
+from arbitrarystyletransfer_amd import mbtrain
+d = np.load(sys.argv[1])
+T = lambda k: torch.from_numpy(d[k]).cuda()
+out = {}
+# weight gradient of a 1x1 conv: dY [n][cout][P] . X^T, the image folded into K (k-contiguous A and B)
+g, x = T('g'), T('x')
+n, cout, P = g.shape
+cin = x.shape[1]
+dw = torch.empty((cout, cin), device='cuda')
+mbtrain.gemm(g, x, dw, cout, cin, n * P, 1, (cout * P, P, 1), (cin * P, 1, P), (0, cin, 1), ksplit=5, fold_k=P)
+out['wgrad'] = dw.cpu().numpy()
+# batched, k-contiguous A only
+A, B = T('A'), T('B')
+C = torch.empty((A.shape[0], A.shape[1], B.shape[2]), device='cuda')
+mbtrain.gemm(A, B, C, A.shape[1], B.shape[2], A.shape[2], A.shape[0], (A.shape[1] * A.shape[2], A.shape[2], 1),
+             (B.shape[1] * B.shape[2], B.shape[2], 1), (A.shape[1] * B.shape[2], B.shape[2], 1))
+out['batched'] = C.cpu().numpy()
+np.savez(sys.argv[2], **out)
+"""
+
+
+def test_mbt_gemm_float4_staging_bit_identical(hip_device, tmp_path):
+    """The float4 k-run staging of the training GEMM (AST_MBGEMM_VEC, csrc/mbtrain.hip) fills the
+    same LDS tiles as the scalar staging: bit-identical products, on a folded-K weight gradient
+    (ragged cout/cin, K split) and a batched product, each run in a child per setting."""
+    import os
+    import subprocess
+    import sys
+    rng = np.random.default_rng(3)
+    f = lambda *s: (rng.random(s, dtype=np.float32) * 2 - 1)  # noqa: E731
+    src = tmp_path / "in.npz"
+    np.savez(src, g=f(3, 40, 1600), x=f(3, 72, 1600), A=f(2, 96, 512), B=f(2, 512, 70))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for vec in ("1", "0"):
+        dst = tmp_path / f"out{vec}.npz"
+        subprocess.run([sys.executable, "-c", _GEMM_CHILD, str(src), str(dst)], cwd=root, check=True, timeout=240,
+                       env=dict(os.environ, AST_MBGEMM_VEC=vec))
+        res.append(np.load(dst))
+    for k in ("wgrad", "batched"):
+        assert np.array_equal(res[0][k], res[1][k]), k
+    ref = np.einsum("ncp,nkp->ck", np.load(src)["g"].astype(np.float64), np.load(src)["x"].astype(np.float64))
+    assert np.abs(res[0]["wgrad"] - ref).max() <= 1e-4 * np.abs(ref).max()
+
+
 @pytest.mark.parametrize("k,s", [(3, 1), (5, 2)])
 def test_dw_and_se_backward(k, s, hip_device):
     torch.manual_seed(0)
