@@ -377,19 +377,38 @@ __global__ __launch_bounds__(256) void border_lines_kernel(const float* __restri
   float acc[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-  for (int c0 = 0; c0 < cout; c0 += BL_CO) {
-    __syncthreads();
-    for (int e = t; e < BL_CO * (BL_Q + 2); e += 256) {
+  // the next cout chunk's line values and weights are loaded into registers while this chunk's FMAs
+  // run (per-thread staging coordinates fixed across chunks)
+  constexpr int ND = (BL_CO * (BL_Q + 2) + 255) / 256, NWT = BL_CO * BL_CI * 3 / 256;
+  static_assert(BL_CO * BL_CI * 3 % 256 == 0, "whole weight items per thread");
+  float dreg[ND], wreg[NWT];
+  auto gload = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      const int e = t + 256 * i;
       const int co = e / (BL_Q + 2), j = e - co * (BL_Q + 2), src = q0 - 2 + j;
-      Ds[co][j] = (c0 + co < cout && src >= 0 && src < L) ? dyn[(int64_t)(c0 + co) * plane + src] : 0.f;
+      dreg[i] = (e < BL_CO * (BL_Q + 2) && c0 + co < cout && src >= 0 && src < L)
+                    ? dyn[(int64_t)(c0 + co) * plane + src] : 0.f;
     }
-    for (int e = t; e < BL_CO * BL_CI * 3; e += 256) {
+#pragma unroll
+    for (int i = 0; i < NWT; ++i) {
+      const int e = t + 256 * i;
       const int co = e / (BL_CI * 3), r = e - co * (BL_CI * 3), cc = r / 3, k = r - 3 * cc;
       // w[co][ci][ky][kx]: rows vary kx at ky = fixed, columns vary ky at kx = fixed
       const int tap = row ? 3 * fixed + k : 3 * k + fixed;
-      Ws[co][cc][k] = (c0 + co < cout && ci0 + cc < cin) ? wt[((int64_t)(c0 + co) * cin + ci0 + cc) * 9 + tap] : 0.f;
+      wreg[i] = (c0 + co < cout && ci0 + cc < cin) ? wt[((int64_t)(c0 + co) * cin + ci0 + cc) * 9 + tap] : 0.f;
     }
+  };
+  gload(0);
+  for (int c0 = 0; c0 < cout; c0 += BL_CO) {
     __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ND; ++i)
+      if (t + 256 * i < BL_CO * (BL_Q + 2)) (&Ds[0][0])[t + 256 * i] = dreg[i];
+#pragma unroll
+    for (int i = 0; i < NWT; ++i) (&Ws[0][0][0])[t + 256 * i] = wreg[i];
+    __syncthreads();
+    if (c0 + BL_CO < cout) gload(c0 + BL_CO);
     const int cn = min(BL_CO, cout - c0);
     for (int co = 0; co < cn; ++co) {
       const float w0 = Ws[co][ci][0], w1 = Ws[co][ci][1], w2 = Ws[co][ci][2];
