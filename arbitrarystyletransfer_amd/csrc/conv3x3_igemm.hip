@@ -2222,6 +2222,11 @@ int ast_conv3x3_dgrad_f32(int cfg, const float* dy, const float* w_tf_packed, fl
   }();
   if (cfg >= 24 && cfg <= 27 && m16 == 1) cfg += 4;
   if (cfg >= 28 && cfg <= 31 && m16 == 0) cfg -= 4;
+#if !X3_STAGED_EPI
+  // the 32x32 kernels' direct-store epilogue (store_tiles) has no input-gradient epilogue: the
+  // caller then runs the plain conv and ast_dgrad_finish_f32
+  if (cfg >= 24 && cfg <= 27) return AST_E_UNSUPPORTED;
+#endif
   const CfgEntry& e = kConfigs[cfg];
   if (sum2 && e.rm % 2 != 0) return AST_E_UNSUPPORTED;
   if (e.bn > kCoutAlign && (cin % e.bn) != 0) return AST_E_UNSUPPORTED;

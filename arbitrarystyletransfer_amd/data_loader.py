@@ -416,15 +416,21 @@ def device_batches(decoded_iter, transform, pairs=True):
             yield torch.stack([transform(c).float() for c in items])
 
 
+def _gpu_initialized():
+    return torch.cuda.is_initialized()
+
+
 def _decoded_loader(dataset, batch_size, num_workers):
     # forked workers (the default start) only while this process has not initialised the GPU: a fork
     # of a HIP-initialised process is not safe, so a caller that touched the GPU first gets spawned
     # workers (they import the package and decode with PIL only)
-    ctx = "spawn" if num_workers > 0 and torch.cuda.is_initialized() else None
+    ctx = "spawn" if num_workers > 0 and _gpu_initialized() else None
     loader = data.DataLoader(HostDecoded(dataset), batch_size=batch_size, sampler=InfiniteSamplerWrapper(dataset),
                              num_workers=num_workers, collate_fn=_collate_list, multiprocessing_context=ctx,
                              persistent_workers=num_workers > 0, prefetch_factor=2 if num_workers > 0 else None)
-    return iter(loader)   # starts the workers now (before the caller touches the GPU)
+    # iter() starts the workers now: forked when the caller builds the iterator before touching the GPU
+    # (as the trainers do), spawned (a fresh interpreter importing this package, no GPU init) otherwise
+    return iter(loader)
 
 
 def content_style_iter(content_dir, style_dir, transform, batch_size, num_workers=4):

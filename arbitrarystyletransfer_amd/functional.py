@@ -62,6 +62,11 @@ def conv_input_grad_same(dy, weight, in_scale=None):
 _E_UNSUPPORTED = -3  # AST_E_UNSUPPORTED (include/ast_hip.h)
 
 
+def dgrad_kind(up):
+    """conv_tuning.json key suffix of an ast_conv3x3_dgrad_f32 launch (scripts/tune_conv.py TUNE_DGRAD)."""
+    return " dgrad sum2" if up == 2 else " dgrad"
+
+
 def conv_input_grad(dy, weight, upsample=1, pad_mode="zeros", in_scale=None, mask=None, add_pre=None,
                     add_post=None):
     """dL/dx of y = conv3x3(pad(upsample(x))) given dL/dy, with the fused input-gradient epilogue of
@@ -93,7 +98,7 @@ def conv_input_grad(dy, weight, upsample=1, pad_mode="zeros", in_scale=None, mas
         code = _E_UNSUPPORTED
         if ops.pack_plan(n, W, False) == (1, 0):
             packed = _TF.get(weight, in_scale)
-            cfg = ops.tuned_config(n, cout, H, W, cin, 1, "zeros", up == 2)
+            cfg = ops.tuned_config(n, cout, H, W, cin, 1, "zeros", False, dgrad_kind(up))
             code = ops._timed(f"conv3x3 dgrad {cout}->{cin} {H}x{W} up{up}", 2 * n * H * W * cout * cin * 9, dy.device,
                               lambda: lib().ast_conv3x3_dgrad_f32(cfg, ptr(dy), ptr(packed), ptr(dx), ptr(mask),
                                                                   ptr(add_pre), ptr(add_post), n, cout, H, W, cin,

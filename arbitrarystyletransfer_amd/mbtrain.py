@@ -46,6 +46,9 @@ def gemm(A, B, C, M, N, K, batch, sA, sB, sC, ksplit=1, accumulate=False, fold_k
         tiles = -(-M // 64) * -(-N // 64) * batch
         if tiles < 256 and K >= 128:
             ksplit = max(1, min(-(-512 // tiles), K // 64))
+            # the C side rounds the chunk up to a multiple of 32 (GK): recount the splits so none is empty
+            kchunk = -(-(-(-K // ksplit)) // 32) * 32
+            ksplit = -(-K // kchunk)
     nws = int(lib().ast_mbt_gemm_workspace_floats(M, N, batch, ksplit, sC[0]))
     ws = workspace(nws, C.device) if nws > 0 else None
     check(ops._timed(f"mbgemm {role} {M}x{N}x{K}", 2 * M * N * K * batch, C.device, lambda: lib().ast_mbt_gemm_f32(

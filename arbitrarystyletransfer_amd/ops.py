@@ -84,9 +84,11 @@ def _dev(t: torch.Tensor, name: str) -> torch.Tensor:
 _TUNING = None
 
 
-def tuned_config(n, cin, h_in, w_in, cout, up, pad_mode, pool) -> int:
+def tuned_config(n, cin, h_in, w_in, cout, up, pad_mode, pool, kind="") -> int:
     """Kernel configuration measured fastest for this shape (scripts/tune_conv.py writes
-    conv_tuning.json); -1 (the library's own heuristic) for shapes never tuned."""
+    conv_tuning.json); -1 (the library's own heuristic) for shapes never tuned. `kind` separates
+    launches of the same GEMM shape with another epilogue (" dgrad": the input-gradient conv of
+    ast_conv3x3_dgrad_f32, " dgrad sum2" with its 2x2-sum upsample adjoint), timed on their own."""
     global _TUNING
     if _TUNING is None:
         import json
@@ -98,7 +100,7 @@ def tuned_config(n, cin, h_in, w_in, cout, up, pad_mode, pool) -> int:
                 _TUNING = json.load(f)
         except (OSError, ValueError):
             _TUNING = {}
-    k = f"{n}x{cin}x{h_in}x{w_in}->{cout} up{up} {pad_mode}{' pool' if pool else ''}"
+    k = f"{n}x{cin}x{h_in}x{w_in}->{cout} up{up} {pad_mode}{' pool' if pool else ''}{kind}"
     return int(_TUNING.get(k, -1))
 
 def pack_conv3x3(weight: torch.Tensor) -> torch.Tensor:

@@ -1,4 +1,6 @@
-"""Debug: LossNetFn vs the per-layer EncoderConvFn chain vs CPU float64, per tap set."""
+"""Debug: LossNetFn vs the per-layer EncoderConvFn chain vs CPU float64, per tap set; beside them
+the CPU's own fp32 evaluation of the same walk against float64 (torch CPU autograd, its own ReLU
+masks and pool argmaxes), i.e. how far fp32 arithmetic alone lands from float64 on that tap set."""
 import sys
 import numpy as np
 import torch
@@ -34,6 +36,21 @@ def run(taps, H=64, W=48):
     gs = [torch.from_numpy((synth.uniform(90 + i, int(np.prod(outs[t].shape))) * 2 - 1).astype(np.float32)
                            .reshape(outs[t].shape)) for i, t in enumerate(taps)]
     sum((outs[t] * g.double()).sum() for t, g in zip(taps, gs)).backward()
+    # CPU fp32 walk, same weights and gradients
+    x32 = x.clone().requires_grad_()
+    cur = R.normalization(x32)
+    o32 = {}
+    k = 0
+    for v in synth.VGG19_CFG:
+        if v == "M":
+            cur = F.max_pool2d(cur, 2, 2); o32[f"pool_{k}"] = cur; continue
+        c = convs[k]; k += 1
+        pre = F.conv2d(cur, c.weight.detach().cpu(), c.bias.detach().cpu(), padding=1)
+        o32[f"conv_{k}"] = pre; cur = F.relu(pre); o32[f"relu_{k}"] = cur
+        if all(t in o32 for t in taps):
+            break
+    sum((o32[t] * g).sum() for t, g in zip(taps, gs)).backward()
+    cpu32 = rel(x32.grad, xr.grad)
     res = []
     for fused in (True, False):
         net.requires_grad_(not fused)
@@ -43,7 +60,7 @@ def run(taps, H=64, W=48):
         res.append(rel(xd.grad, xr.grad))
         if not fused:
             net.zero_grad(set_to_none=True)
-    print(f"{str(taps):60s} fused {res[0]:.2e} chain {res[1]:.2e}", flush=True)
+    print(f"{str(taps):60s} fused {res[0]:.2e} chain {res[1]:.2e} cpu_fp32 {cpu32:.2e}", flush=True)
 
 
 for taps in [("relu_1",), ("relu_1", "relu_2"), ("relu_2",), ("conv_2",), ("relu_1", "conv_3"), ("relu_3",),

@@ -114,8 +114,89 @@ def ast_shapes(batch=8, size=160):
     return seen
 
 
-def key(n, cin, h, w, cout, up, pad, pool):
-    return f"{n}x{cin}x{h}x{w}->{cout} up{up} {pad}{' pool' if pool else ''}"
+def key(n, cin, h, w, cout, up, pad, pool, kind=""):
+    return f"{n}x{cin}x{h}x{w}->{cout} up{up} {pad}{' pool' if pool else ''}{kind}"
+
+
+def dgrad_shapes(mode):
+    """The fused input-gradient launches (ast_conv3x3_dgrad_f32) of one training step of `mode`
+    ("train" = config 3, "ast", "ae"): (n, cout, H, W, cin, up, has_mask, has_pre, has_post), captured
+    by spying functional.conv_input_grad in a live step."""
+    from arbitrarystyletransfer_amd import functional as Fn
+    seen = []
+    orig = Fn.conv_input_grad
+
+    def spy(dy, weight, upsample=1, pad_mode="zeros", in_scale=None, mask=None, add_pre=None, add_post=None):
+        n, cout, H, W = (int(v) for v in dy.shape)
+        fused = upsample == 2 or mask is not None or add_pre is not None or add_post is not None
+        if fused and ops.pack_plan(n, W, False) == (1, 0):
+            shp = (n, cout, H, W, int(weight.shape[1]), int(upsample), mask is not None, add_pre is not None,
+                   add_post is not None)
+            if shp not in seen:
+                seen.append(shp)
+        return orig(dy, weight, upsample, pad_mode, in_scale, mask, add_pre, add_post)
+
+    Fn.conv_input_grad = spy
+    try:
+        {"train": adain_train_shapes, "ast": ast_shapes, "ae": ae_shapes}[mode]()
+    finally:
+        Fn.conv_input_grad = orig
+    return seen
+
+
+def time_dgrad(cfg, dy, packed, dx, mask, ap, aq, shp):
+    from arbitrarystyletransfer_amd._lib import ptr, stream_ptr
+    n, cout, H, W, cin, up = shp[:6]
+
+    def launch():
+        return lib().ast_conv3x3_dgrad_f32(cfg, ptr(dy), ptr(packed), ptr(dx), ptr(mask), ptr(ap), ptr(aq), n, cout, H,
+                                           W, cin, up, stream_ptr(dy.device))
+    if launch() != 0:
+        return None
+    for _ in range(2):
+        launch()
+    ts = []
+    for _ in range(5):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        launch()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    return statistics.median(ts)
+
+
+def tune_dgrad(mode, table, ncfg):
+    """TUNE_DGRAD=train|ast|ae: time every configuration of each fused input-gradient launch of that
+    training step; keys carry functional.dgrad_kind's suffix."""
+    from arbitrarystyletransfer_amd import functional as Fn
+    dev = torch.device("cuda:0")
+    report = []
+    for shp in dgrad_shapes(mode):
+        n, cout, H, W, cin, up, hm, hp, hq = shp
+        h, w = H // up, W // up
+        dy = torch.from_numpy(synth.image(7, (n, cout, H, W))).to(dev)
+        wt = torch.from_numpy(synth.conv_weight(8, cout, cin, 3)).to(dev)
+        packed = Fn._TF.get(wt)
+        dx = torch.empty((n, cin, h, w), device=dev)
+        side = lambda on, seed: torch.from_numpy(synth.image(seed, (n, cin, h, w))).to(dev) if on else None  # noqa: E731
+        mask, ap, aq = side(hm, 9), side(hp, 10), side(hq, 11)
+        res = {}
+        for cfg in range(ncfg):
+            t = time_dgrad(cfg, dy, packed, dx, mask, ap, aq, shp)
+            if t is not None:
+                res[cfg] = t
+        if not res:
+            continue
+        best = min(res, key=res.get)
+        k = key(n, cout, H, W, cin, 1, "zeros", False, Fn.dgrad_kind(up))
+        table[k] = best
+        flops = 2 * n * H * W * cout * cin * 9
+        row = {"shape": k, "best": best, "ms": res[best], "tflops": flops / res[best] / 1e9,
+               "all_ms": {str(c): round(t, 4) for c, t in res.items()}}
+        report.append(row)
+        print(json.dumps(row), flush=True)
+    return report
 
 
 def time_cfg(cfg, x, wp, b, cout, up, pad, pool):
@@ -148,12 +229,16 @@ def main():
     if os.path.exists(path):
         table = json.load(open(path))
     report = []
-    todo = ae_shapes() if os.environ.get("TUNE_AE") else adain_train_shapes() if os.environ.get("TUNE_TRAIN") \
-        else ast_shapes() if os.environ.get("TUNE_AST") else shapes(batch)
-    if os.environ.get("TUNE_NEW"):  # only shapes the table does not hold yet
-        todo = [t for t in todo if key(*t) not in table]
-    if os.environ.get("TUNE_SMALL"):  # only the shapes the direct VALU kernels serve (cin or cout <= 4)
-        todo = [t for t in todo if t[1] <= 4 or t[4] <= 4]
+    if os.environ.get("TUNE_DGRAD"):
+        report = tune_dgrad(os.environ["TUNE_DGRAD"], table, ncfg)
+        todo = []
+    else:
+        todo = ae_shapes() if os.environ.get("TUNE_AE") else adain_train_shapes() if os.environ.get("TUNE_TRAIN") \
+            else ast_shapes() if os.environ.get("TUNE_AST") else shapes(batch)
+        if os.environ.get("TUNE_NEW"):  # only shapes the table does not hold yet
+            todo = [t for t in todo if key(*t) not in table]
+        if os.environ.get("TUNE_SMALL"):  # only the shapes the direct VALU kernels serve (cin or cout <= 4)
+            todo = [t for t in todo if t[1] <= 4 or t[4] <= 4]
     for shp in todo:
         n, cin, h, w, cout, up, pad, pool = shp
         x = torch.from_numpy(synth.image(5, (n, cin, h, w))).to(dev)

@@ -65,3 +65,24 @@ def test_host_decoded_matches_dataset_item(tmp_path):
     torch.manual_seed(7)
     c2, s2 = ds[0]
     assert np.array_equal(c1, np.asarray(c2)) and np.array_equal(s1, np.asarray(s2))
+
+
+def test_spawned_workers_after_gpu_init(tmp_path, monkeypatch):
+    """A caller that initialised the GPU before building the iterator gets spawned workers
+    (data_loader._decoded_loader): HostDecoded and the dataset pickle into a fresh interpreter that
+    imports the package and decodes with PIL only. The GPU init is stubbed (CPU host)."""
+    content = _write_images(tmp_path / "content", 3, 6)
+    monkeypatch.setattr(DL, "_gpu_initialized", lambda: True)
+    seen = {}
+    orig = DL.data.DataLoader
+
+    def spy(*a, **kw):
+        seen["ctx"] = kw.get("multiprocessing_context")
+        return orig(*a, **kw)
+    monkeypatch.setattr(DL.data, "DataLoader", spy)
+    it = DL.content_iter([str(tmp_path / "content")], _host_to_tensor, batch_size=2, num_workers=1)
+    assert seen["ctx"] == "spawn"
+    b = next(it)
+    assert b.shape == (2, 3, 10, 12)
+    for k in range(2):
+        assert len(_find(b[k], content)) == 1
