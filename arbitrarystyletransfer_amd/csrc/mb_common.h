@@ -55,6 +55,10 @@ inline bool ed_plan(EdArgs& a, long long slots) {
 // is outside that set (the caller falls back to v3 / v1).
 int launch_ed4(EdArgs a, int k, int stride, hipStream_t st);
 
+// v5 (mb_ed5.hip: bf16 expand blocks, k 5, stride 1, cin_pad <= 48, wo % 4 == 0): the depthwise on
+// the matrix cores (Toeplitz form); AST_E_UNSUPPORTED outside that set (the caller runs v4).
+int launch_ed5(EdArgs a, int k, int stride, hipStream_t st);
+
 // 1 if launch_edpw4 runs this block shape (bf16, k 3, stride 1, no upsample, c1 == cin), else 0.
 int edpw4_supported(int cin_pad, int hid, int cout, int k, int stride, int up, int ho, int wo);
 int launch_edpw4(const EdpwArgs& a, hipStream_t st);

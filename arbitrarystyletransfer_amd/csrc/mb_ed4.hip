@@ -4,6 +4,7 @@
 // independent taps bought no throughput and cost ~120 register shuffles per input row.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "../../include/ast_hip.h"
 #include "mb_common.h"
 
@@ -893,7 +894,17 @@ int launch_ed4(EdArgs a, int k, int stride, hipStream_t st) {
     return AST_E_UNSUPPORTED;
   }
   if (k == 3) return launch_k<3>(a, st);
-  if (k == 5) return launch_k<5>(a, st);
+  if (k == 5) {
+    static const int v5 = [] {  // AST_MB_ED5=0: the v4 k5 kernels (A/B measurements)
+      const char* v = getenv("AST_MB_ED5");
+      return v ? atoi(v) : 1;
+    }();
+    if (v5) {
+      const int r = launch_ed5(a, k, stride, st);
+      if (r != AST_E_UNSUPPORTED) return r;
+    }
+    return launch_k<5>(a, st);
+  }
   return AST_E_UNSUPPORTED;
 }
 

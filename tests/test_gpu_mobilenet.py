@@ -57,6 +57,11 @@ BLOCKS = [
     (36, 36, 1, 3, 5, True, True, (1, 19, 70), 1),     # hidden 108, k5, ragged tiles both ways
     (20, 24, 2, 6, 3, False, True, (2, 70, 92), 1),    # stride 2: hidden 120, 4 strips, odd output height
     (24, 40, 2, 6, 5, True, True, (1, 66, 124), 1),    # k5 stride 2: 2 bands of output rows, 5 strips
+    # k5 stride 1 with cin <= 48 and W % 4 == 0: the MFMA depthwise (v5, csrc/mb_ed5.hip)
+    (40, 40, 1, 4, 5, False, True, (2, 70, 60), 1),    # 3 bands (last ragged), last strip 4 columns wide
+    (40, 24, 1, 6, 5, True, True, (1, 33, 100), 1),    # hidden 240: a half-filled last 32-channel chunk
+    (24, 24, 1, 6, 5, False, True, (1, 5, 8), 1),      # map smaller than one tile (reflect on 5 rows)
+    (16, 16, 1, 4, 5, True, True, (2, 32, 28), 1),     # exactly one tile, one K-step
 ]
 
 
