@@ -17,9 +17,9 @@
 //     hidden row n + ky -- one ds_read_b128 from the [channel][row][col] LDS image, row pitch 80 B
 //     (conflict-free for the b128 lane groups);
 //   A (Toeplitz weights, M = output column): lane (m, g) needs the 8 entries s..s+7 of the channel's
-//     zero-padded kernel row R_ky (R[t] = w[ky][t - 31]), s = 16 w + 8 g - m + 31; a second copy
-//     shifted by one element makes every start 4-byte aligned (4 x ds_read_b32; the copy sits 704 B
-//     after the first so the two halves of a lane group fall on disjoint banks).
+//     zero-padded kernel row R_ky (R[t] = w[ky][t - 31]), s = 16 w + 8 g - m + 31; eight copies of
+//     the row's nonzero neighbourhood, each shifted by one element, make every window one aligned
+//     ds_read_b128 (4 x ds_read_b32 from two copies ran LDS-bound at two waves per SIMD).
 // The hidden values are rounded to bf16 (the MFMA operand) and so are the folded depthwise weights:
 // a bf16 model's own tensors (the reference in bf16 stores the expand output as bf16); accumulation
 // is fp32. The tests bound the block against the fp32 oracle at the bf16 bar.
@@ -80,12 +80,11 @@ constexpr int OW = 28;             // output columns per tile (M = 32, the last 
 constexpr int IR = TH + K5 - 1;    // 36 input rows
 constexpr int RP = 80;             // hidden row pitch (bytes): 16 * odd -> conflict-free B reads
 constexpr int CP = IR * RP + 16;   // channel pitch 2896 B: CP / 4 = 4 * odd mod 32 -> conflict-free writes
-constexpr int R1OFF = 704;         // second (shifted) copy of the Toeplitz rows
-constexpr int TP = R1OFF + 5 * 128;  // Toeplitz table bytes per channel (1344)
+constexpr int TP = 5 * 8 * 32;     // Toeplitz table bytes per channel: [ky][copy 0..7][16 bf16]
 constexpr int NCH = 32;            // hidden channels per chunk
 constexpr int NW = 8;              // waves per workgroup
 constexpr int LDS_H = NCH * CP;    // 92,672
-constexpr int LDS_T = NCH * TP;    // 43,008
+constexpr int LDS_T = NCH * TP;    // 40,960
 constexpr int NT = (IR + NW - 1) / NW;  // input-row slots per wave (5)
 
 template <int KS>
@@ -123,7 +122,9 @@ __global__ __launch_bounds__(64 * NW, 2) void expand_dw5_kernel(EdArgs a, int st
 #pragma unroll
       for (int q = 0; q < KS; ++q)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) raw[q][e] = __builtin_amdgcn_raw_buffer_load_b16(xr, vrow + (16 * q + e) * hw2, 0, 0);
+        for (int e = 0; e < 8; ++e)
+          raw[q][e] = (ED5_SKIP & 32) ? (unsigned)(vrow + q + e) & 0x3f3fu
+                                      : __builtin_amdgcn_raw_buffer_load_b16(xr, vrow + (16 * q + e) * hw2, 0, 0);
 #pragma unroll
       for (int q = 0; q < KS; ++q) {
         u32x4 f;
@@ -136,11 +137,17 @@ __global__ __launch_bounds__(64 * NW, 2) void expand_dw5_kernel(EdArgs a, int st
 
   // depthwise operand offsets: A (Toeplitz) start s = 16 w + 8 h - r + 31, from the copy that makes it
   // 4-byte aligned; B lane (row r, k-group h) at r * RP + 16 h
+  // The 8 entries s..s+7 are all zero unless s is in [24, 35]; the other windows read entries 36..43
+  // (zeros), so every window lies in R[24..43]. Copy k of a kernel row holds R[24 + k .. 39 + k]: the
+  // window starting at s comes from copy s & 7 at entry s - (s & 7) - 24 (0 or 8), a 16-byte-aligned
+  // ds_read_b128; the 16 distinct (copy, half) slots of a row are 256 B, so a lane group reads
+  // conflict-free (identical windows broadcast).
   int aoff[2];
 #pragma unroll
   for (int w = 0; w < 2; ++w) {
-    const int st = 16 * w + 8 * h - r + 31;
-    aoff[w] = (st & 1) ? R1OFF + 2 * (st - 1) : 2 * st;
+    int st = 16 * w + 8 * h - r + 31;
+    st = (st < 24 || st > 35) ? 36 : st;
+    aoff[w] = 32 * (st & 7) + 2 * (st - (st & 7) - 24);
   }
   const int boff = r * RP + 16 * h;
 
@@ -186,13 +193,13 @@ __global__ __launch_bounds__(64 * NW, 2) void expand_dw5_kernel(EdArgs a, int st
     for (int u = 0; u < 4; ++u)
       cw.bd[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bdr, 4 * (cb * NCH + wv * 4 + u), 0, 0));
   };
-  auto write_t = [&](int it, float v) {  // Toeplitz rows: R0[ky][31 + kx], R1[ky][30 + kx]
+  auto write_t = [&](int it, float v) {  // weight (ky, kx) of a channel into its 8 copies: copy k entry 7 + kx - k
     const int c = it / 25, t = it - 25 * c, ky = t / 5, kx = t - 5 * ky;
     const unsigned short b = bits16(v);
-    reinterpret_cast<unsigned short*>(Ts + c * TP + ky * 128)[31 + kx] = b;
-    reinterpret_cast<unsigned short*>(Ts + c * TP + R1OFF + ky * 128)[30 + kx] = b;
+    unsigned short* row = reinterpret_cast<unsigned short*>(Ts + c * TP + ky * 256) + 7 + kx;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) row[16 * k - k] = b;
   };
-
   ChunkW cur;
   load_chunk(0, cur);
   // wait for every load before the loop: otherwise the wait-count analysis merges the loop entry (loads
@@ -252,8 +259,8 @@ __global__ __launch_bounds__(64 * NW, 2) void expand_dw5_kernel(EdArgs a, int st
 #pragma unroll
         for (int w = 0; w < 2; ++w) {
           if (ED5_SKIP & 2) continue;
-          const unsigned* ap = reinterpret_cast<const unsigned*>(tb + ky * 128 + aoff[w]);
-          const u32x4 af = (ED5_SKIP & 8) ? u32x4{(unsigned)aoff[w], 0u, 1u, 2u} : u32x4{ap[0], ap[1], ap[2], ap[3]};
+          const u32x4 af = (ED5_SKIP & 8) ? u32x4{(unsigned)aoff[w], 0u, 1u, 2u}
+                                          : *reinterpret_cast<const u32x4*>(tb + ky * 256 + aoff[w]);
           const u32x4 bf = *reinterpret_cast<const u32x4*>(hb + ky * RP + 32 * w);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af), __builtin_bit_cast(bf16x8, bf),
                                                         acc, 0, 0, 0);
