@@ -1073,20 +1073,10 @@ __global__ __launch_bounds__(kThreads) void se_fold_kernel(const float* __restri
   const int n = blockIdx.x;
   for (int c = threadIdx.x; c < hid; c += kThreads) mean[c] = pool[(int64_t)n * hid + c] / hw;
   __syncthreads();
-  // FC1 as one wave per output: lanes stride the hidden channels, the partial sums meet in a fixed
-  // shuffle order (deterministic). One thread per output with a serial hid-long loop left most of
-  // the workgroup idle and took ~50 us per launch (46 launches per config-5 step).
-  {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    constexpr int NWV = kThreads / 64;
-#pragma unroll 2
-    for (int j = wv; j < red; j += NWV) {
-      float s = 0.f;
-      for (int c = lane; c < hid; c += 64) s = fmaf(fc1w[(int64_t)j * hid + c], mean[c], s);
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-      if (lane == 0) hmid[j] = fmaxf(fc1b[j] + s, 0.f);
-    }
+  for (int j = threadIdx.x; j < red; j += kThreads) {
+    float s = fc1b[j];
+    for (int c = 0; c < hid; ++c) s = fmaf(fc1w[(int64_t)j * hid + c], mean[c], s);
+    hmid[j] = fmaxf(s, 0.f);
   }
   __syncthreads();
   for (int c = threadIdx.x; c < hid; c += kThreads) {
@@ -1095,10 +1085,14 @@ __global__ __launch_bounds__(kThreads) void se_fold_kernel(const float* __restri
     gate[c] = fminf(fmaxf(s, 0.f), 1.f);
   }
   __syncthreads();
+  // the gated weights row by row: a wave per output channel, lanes along the hidden channels (the
+  // flat form paid an integer division per element: ~75 us per launch, 46 launches per config-5 step)
   T* o = wg + (int64_t)n * cout_pad * hid_pad;
-  for (int e = threadIdx.x; e < cout_pad * hid_pad; e += kThreads) {
-    const int co = e / hid_pad, c = e - co * hid_pad;
-    o[e] = from_f<T>(co < cout && c < hid ? w2[(int64_t)co * hid + c] * gate[c] : 0.f);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int co = wv; co < cout_pad; co += kThreads / 64) {
+    const float* wr = w2 + (int64_t)co * hid;
+    T* orow = o + (int64_t)co * hid_pad;
+    for (int c = lane; c < hid_pad; c += 64) orow[c] = from_f<T>(co < cout && c < hid ? wr[c] * gate[c] : 0.f);
   }
 }
 
