@@ -354,6 +354,14 @@ def mobilenet_bench(args, dev, rank, world):
     achieved = fused_min_bytes / step_s / 1e9
     # PMC bytes per expand_dw launch, measured at the default B=32, 1024^2
     mb_traffic = _pmc_traffic("mb_traffic.json") if (B, S) == (32, 1024) and not args.attention else (None, None)
+    step_pmc = (None, None)
+    if (B, S) == (32, 1024) and not args.attention:
+        try:
+            with open(os.path.join(ROOT, "profiles", "r06p_mb_step_traffic.json")) as f:
+                d = json.load(f)
+            step_pmc = (d["hbm_gb_per_step"], "profiles/r06p_mb_step_traffic.json (" + d["source"] + ")")
+        except (OSError, ValueError, KeyError):
+            pass
     ed = fam.get("mb expand_dw")
     ed_gbs = (ed[0] / (ed[1] * 1e-3) / 1e9) if ed else None
     dw_tf = (2 * dw_fma_per_step * args.steps / (ed[1] * 1e-3) / 1e12) if ed else None
@@ -368,10 +376,12 @@ def mobilenet_bench(args, dev, rank, world):
                                f"{'AdaAttN' if args.attention else 'AdaIN'}@[12,14] -> ada_out -> "
                                f"Decoder(exporting), bs={B}/GPU {S}x{S}, bf16 storage / fp32 accumulate",
                    "global_batch": B * world, "image_size": S, "parallelism": f"batch-sharded x{world}"},
-        # dominant kernel: the fused expand + depthwise launches (~70% of the step); algorithmic bytes
-        # = its input read + depthwise-output write. It is issue/latency-bound on the depthwise VALU
-        # FMAs rather than on HBM: "valu" gives their rate against the 157.3 TF fp32 vector peak.
-        "roofline": {"bound": "hbm", "kernel": "mb expand_dw (expand 1x1 MFMA + depthwise kxk VALU, all launches)",
+        # dominant kernel: the fused expand + depthwise launches (~60% of the step); algorithmic bytes
+        # = its input read + depthwise-output write. The depthwise runs on the VALU (v4) or, for the k5
+        # blocks with cin <= 48, as a Toeplitz product on the bf16 MFMA (v5, csrc/mb_ed5.hip); "valu"
+        # gives the depthwise MAC rate of the family against the 157.3 TF fp32 vector peak.
+        "roofline": {"bound": "hbm", "kernel": "mb expand_dw (expand 1x1 MFMA + depthwise kxk on VALU (v4) or "
+                                               "Toeplitz MFMA (v5 k5), all launches)",
                      "achieved": ed_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": (ed_gbs / PEAK_HBM_GBS) if ed_gbs else None,
                      # PMC bytes per expand_dw launch, measured at the default B=32, 1024^2
@@ -381,7 +391,9 @@ def mobilenet_bench(args, dev, rank, world):
                      "valu": {"dw_tflops": dw_tf, "peak": PEAK_FP32_MFMA_TF,
                               "frac": (dw_tf / PEAK_FP32_MFMA_TF) if dw_tf else None},
                      "whole_step": {"fused_min_gb_per_step": fused_min_bytes / 1e9, "achieved_gbs": achieved,
-                                    "frac": achieved / PEAK_HBM_GBS},
+                                    "frac": achieved / PEAK_HBM_GBS,
+                                    # every dispatch's FETCH_SIZE x2 + WRITE_SIZE per step, committed PMC run
+                                    "pmc_gb_per_step": step_pmc[0], "pmc_source": step_pmc[1]},
                      "kernel_share_of_step": sum(m for _, _, m in recs) / args.steps / (step_s * 1e3)},
         "kernels": kernels,
     }
