@@ -37,7 +37,6 @@
 // Two barriers per chunk; 136 KB of LDS, one workgroup (two waves per SIMD) per CU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 #include "../../include/ast_hip.h"
 #include "mb_common.h"
 
@@ -335,247 +334,6 @@ int launch_ks5(EdArgs a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// ------------------------------------------------------------------------------------------------
-// v6: the same arithmetic as v5 (expand on 32x32x16 MFMA, bf16 hidden image, 5x5 Toeplitz depthwise on
-// 32x32x16 MFMA, D staged through LDS), reorganised as a two-stage pipeline inside the workgroup. v5
-// ran its phases one after the other behind two barriers per chunk, and PMC showed its waves waiting
-// 36% of their cycles on barriers / counters and stalled on issue another 31%, with the MFMA pipe busy
-// 22% (profiles/r06g_pmc_ed5.txt). Here waves 0-3 (producers) expand half-chunk i (16 hidden channels)
-// into LDS buffer i & 1 while waves 4-7 (consumers) run the depthwise and epilogue of half-chunk i - 1
-// from the other buffer; one barrier per step. Waves w and w + 4 share a SIMD (a workgroup's waves are
-// dealt to SIMDs cyclically), so every SIMD holds one wave of each stage and their VALU, MFMA and LDS
-// work interleave. Each producer keeps the x fragments of its 9 input rows in registers for the
-// tile; the expand MFMA's other 16 output columns are unused (the half-chunk is 16 channels: two
-// buffers of the 32-channel image would not fit the LDS). The consumers read nothing from global
-// memory (the depthwise biases come through LDS with the Toeplitz rows), so their stores never hold
-// up a wait. Same products, roundings and order as v5: bit-identical to it.
-constexpr int HC = 16;                  // hidden channels per half-chunk
-constexpr int LDS_H6 = HC * CP;         // 46,336 per buffer
-constexpr int LDS_T6 = HC * TP;         // 20,480 per buffer
-constexpr int NP = NW / 2;              // producer waves (= consumer waves)
-constexpr int NT6 = IR / NP;            // input rows per producer wave (9)
-static_assert(IR % NP == 0, "whole rows per producer");
-
-template <int KS>
-__global__ __launch_bounds__(64 * NW, 2) void expand_dw6_kernel(EdArgs a, int strips, int bands, int nhc, int total) {
-  __shared__ __align__(16) unsigned char lds[2 * LDS_H6 + 2 * LDS_T6 + 2 * HC * 4];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
-  const bool prod = wv < NP;  // wave-uniform role
-  const int pw = wv & (NP - 1);
-  unsigned char* const Tb0 = lds + 2 * LDS_H6;
-  float* const bdl = reinterpret_cast<float*>(lds + 2 * LDS_H6 + 2 * LDS_T6);  // [2][HC] depthwise biases
-  // XCD-aware order (workgroup b runs on XCD b % 8): consecutive tiles of an image row band share an L2
-  const int per = (total + 7) >> 3;
-  const int L = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-  if (L >= total) return;  // uniform over the workgroup
-  const int s = L % strips;
-  const int rest = L / strips;
-  const int band = rest % bands, n = rest / bands;
-  const int x0 = s * OW - P5, y0 = band * TH;
-  constexpr unsigned kDrop = 0x80000000u;
-
-  for (int i = tid; i < 2 * LDS_T6 / 16; i += 64 * NW) reinterpret_cast<uint4*>(Tb0)[i] = make_uint4(0u, 0u, 0u, 0u);
-
-  // ---- producer state: x fragments of rows j = pw + 4 t, expand parameters one half-chunk ahead
-  const int hw2 = 2 * a.h * a.w;
-  const int hid16 = (a.hid + 15) / 16 * 16;
-  bf16x8 xa[NT6][KS];
-  const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w1), 0,
-                                                                       2 * hid16 * a.cin_pad, 0x00020000);
-  const __amdgpu_buffer_rsrc_t b1r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.b1), 0, 4 * a.hid, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wdr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.wdw), 0, 100 * a.hid, 0x00020000);
-  const __amdgpu_buffer_rsrc_t bdr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.bdw), 0, 4 * a.hid, 0x00020000);
-  struct PW {
-    bf16x8 bw[KS];
-    float b1, wt0, wt1, bd;
-  };
-  const int ptid = tid & (64 * NP - 1);               // producer thread 0..255
-  const int pit1 = min(ptid + 64 * NP, HC * 25 - 1);  // its second Toeplitz item (if < 400)
-  auto load_pw = [&](int i, PW& p) {
-    // expand B columns: lane r < 16 = hidden channel i * 16 + r; the other 16 read out of range (0)
-    const int ch = i * HC + r;
-#pragma unroll
-    for (int q = 0; q < KS; ++q) {
-      const unsigned off = r < HC ? (unsigned)(2 * (ch * a.cin_pad + 16 * q + 8 * h)) : kDrop;
-      p.bw[q] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w1r, (int)off, 0, 0));
-    }
-    p.b1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b1r, r < HC ? 4 * ch : (int)kDrop, 0, 0));
-    p.wt0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wdr, 4 * (i * HC * 25 + ptid), 0, 0));
-    p.wt1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wdr, 4 * (i * HC * 25 + pit1), 0, 0));
-    p.bd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bdr, 4 * (i * HC + min(ptid, HC - 1)), 0, 0));
-  };
-  PW cur;
-  if (prod) {
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<bf16*>(reinterpret_cast<const bf16*>(a.x1) + (int64_t)n * a.cin * (hw2 / 2)), 0, a.cin * hw2,
-        0x00020000);
-    const int pc = 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3);  // C rows of a lane half = 16 consecutive columns
-    const int gx = refl5(x0 + pc, a.w);
-#pragma unroll
-    for (int t = 0; t < NT6; ++t) {
-      const int vrow = 8 * h * hw2 + 2 * (refl5(y0 - P5 + pw + NP * t, a.h) * a.w + gx);
-      unsigned raw[KS][8];
-#pragma unroll
-      for (int q = 0; q < KS; ++q)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) raw[q][e] = __builtin_amdgcn_raw_buffer_load_b16(xr, vrow + (16 * q + e) * hw2, 0, 0);
-#pragma unroll
-      for (int q = 0; q < KS; ++q) {
-        u32x4 f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) f[e] = (raw[q][2 * e] & 0xffffu) | (raw[q][2 * e + 1] << 16);
-        xa[t][q] = __builtin_bit_cast(bf16x8, f);
-      }
-    }
-    load_pw(0, cur);
-  }
-  auto write_t = [&](unsigned char* tb, int it, float v) {  // copy k of row (c, ky) holds w[ky][kx] at 7 + kx - k
-    const int c = it / 25, t = it - 25 * c, ky = t / 5, kx = t - 5 * ky;
-    const unsigned short b = bits16(v);
-    unsigned short* row = reinterpret_cast<unsigned short*>(tb + c * TP + ky * 256) + 7 + kx;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) row[16 * k - k] = b;
-  };
-
-  // ---- consumer state: operand offsets (as v5) and output geometry
-  int aoff[2];
-#pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    int st = 16 * w + 8 * h - r + 31;
-    st = (st < 24 || st > 35) ? 36 : st;
-    aoff[w] = 32 * (st & 7) + 2 * (st - (st & 7) - 24);
-  }
-  const int boff = r * RP + 16 * h;
-  const int64_t plane_o = (int64_t)a.ho * a.wo;
-  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<bf16*>(a.d) + (int64_t)n * a.hid * plane_o, 0, (int)(2 * a.hid * plane_o), 0x00020000);
-  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
-      a.pool + (int64_t)n * a.hid * a.slots, 0, 4 * a.hid * a.slots, 0x00020000);
-  const bool rowv = y0 + r < a.ho;
-  const bool edge = s * OW + OW > a.wo;
-
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see v5
-  lds_barrier();
-  for (int i = 0; i <= nhc; ++i) {
-    if (prod) {
-      if (i < nhc) {
-        const int b = i & 1;
-        unsigned char* const Hb = lds + b * LDS_H6;
-        unsigned char* const Tb = Tb0 + b * LDS_T6;
-        write_t(Tb, ptid, cur.wt0);
-        if (ptid + 64 * NP < HC * 25) write_t(Tb, ptid + 64 * NP, cur.wt1);
-        if (ptid < HC) bdl[b * HC + ptid] = cur.bd;
-        // the next half-chunk's parameters, a whole step ahead of their use
-        PW nxt;
-        load_pw(i + 1, nxt);  // past the last half-chunk every read is out of range (0), never used
-        // expand, three rows at a time (their MFMAs before their activations)
-#pragma unroll
-        for (int t0 = 0; t0 < NT6; t0 += 3) {
-          f32x16 ce[3];
-#pragma unroll
-          for (int t = 0; t < 3; ++t) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) ce[t][e] = cur.b1;
-#pragma unroll
-            for (int q = 0; q < KS; ++q) ce[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[t0 + t][q], cur.bw[q], ce[t], 0, 0, 0);
-          }
-#pragma unroll
-          for (int t = 0; t < 3; ++t) {
-            unsigned pk[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) pk[e] = pack2(hswish5(ce[t][2 * e]), hswish5(ce[t][2 * e + 1]));
-            if (r < HC) {
-              uint4* dst = reinterpret_cast<uint4*>(Hb + r * CP + (pw + NP * (t0 + t)) * RP + 32 * h);
-              dst[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-              dst[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-            }
-          }
-        }
-        cur = nxt;
-      }
-    } else if (i >= 1) {
-      const int b = (i - 1) & 1, hc0 = (i - 1) * HC;
-      unsigned char* const Hb = lds + b * LDS_H6;
-      unsigned char* const Tb = Tb0 + b * LDS_T6;
-      float psum[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int c = pw * 4 + u, ch = hc0 + c;
-        const float bd = bdl[b * HC + c];
-        f32x16 acc;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = bd;
-        const unsigned char* tb = Tb + c * TP;
-        const unsigned char* hb = Hb + c * CP + boff;
-#pragma unroll
-        for (int ky = 0; ky < K5; ++ky) {
-#pragma unroll
-          for (int w = 0; w < 2; ++w) {
-            const u32x4 af = *reinterpret_cast<const u32x4*>(tb + ky * 256 + aoff[w]);
-            const u32x4 bf = *reinterpret_cast<const u32x4*>(hb + ky * RP + 32 * w);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af), __builtin_bit_cast(bf16x8, bf),
-                                                          acc, 0, 0, 0);
-          }
-        }
-        float y[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) y[e] = hswish5(acc[e]);
-        float t = 0.f;
-        if (!edge) {
-#pragma unroll
-          for (int e = 0; e < 12; ++e) t += y[e];
-          if (h == 0) t += (y[12] + y[13]) + (y[14] + y[15]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int m = 8 * (e >> 2) + 4 * h + (e & 3);
-            t += (m < OW && s * OW + m < a.wo) ? y[e] : 0.f;
-          }
-        }
-        psum[u] = rowv ? t : 0.f;
-        unsigned char* stg = Hb + c * CP;  // this channel's consumed hidden image (see v5)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (q < 3 || h == 0)
-            *reinterpret_cast<u32x2*>(stg + r * 56 + (2 * q + h) * 8) =
-                u32x2{pack2(y[4 * q], y[4 * q + 1]), pack2(y[4 * q + 2], y[4 * q + 3])};
-        }
-        const bool chv = ch < a.hid;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int e = lane + 64 * k, row = e / 7, pc7 = e - 7 * row, col = s * OW + 4 * pc7;
-          const u32x2 v = *reinterpret_cast<const u32x2*>(stg + 8 * min(e, 223));
-          const bool ok = chv && e < 224 && y0 + row < a.ho && col + 4 <= a.wo;
-          const unsigned off = ok ? (unsigned)(2 * ((int64_t)ch * plane_o + (int64_t)(y0 + row) * a.wo + col)) : kDrop;
-          __builtin_amdgcn_raw_buffer_store_b64(v, dr, (int)off, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float v = psum[u];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        const int ch = hc0 + pw * 4 + u;
-        const unsigned off = lane == 0 && ch < a.hid ? (unsigned)(4 * (ch * a.slots + band * strips + s)) : kDrop;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), pr, (int)off, 0, 0);
-      }
-    }
-    lds_barrier();  // buffer i & 1 is written, buffer (i - 1) & 1 is consumed
-  }
-}
-
-template <int KS>
-int launch_ks6(EdArgs a, hipStream_t st) {
-  const int strips = (a.wo + OW - 1) / OW, bands = (a.ho + TH - 1) / TH, nhc = (a.hid + HC - 1) / HC;
-  const int64_t total = (int64_t)strips * bands * a.n;
-  if (total > 0x7ffffff0LL) return AST_E_SHAPE;
-  if (ed_plan(a, (int64_t)bands * strips)) return 0;
-  const int64_t grid = (total + 7) / 8 * 8;
-  hipLaunchKernelGGL((expand_dw6_kernel<KS>), dim3((unsigned)grid), dim3(64 * NW), 0, st, a, strips, bands, nhc,
-                     (int)total);
-  return (int)hipGetLastError();
-}
-
 }  // namespace
 
 int launch_ed5(EdArgs a, int k, int stride, hipStream_t st) {
@@ -585,22 +343,10 @@ int launch_ed5(EdArgs a, int k, int stride, hipStream_t st) {
   if (a.cin_pad % 16 != 0 || a.cin_pad > 48 || a.wo % 4 != 0 || a.ho < 3 || a.wo < 3) return AST_E_UNSUPPORTED;
   if ((int64_t)a.cin_pad * 2 * a.h * a.w >= 0x7fffffffLL || (int64_t)a.hid * 2 * a.ho * a.wo >= 0x7fffffffLL)
     return AST_E_UNSUPPORTED;
-  static const int ver = [] {  // AST_MB_ED5=1: v5 (phases behind two barriers per chunk); default v6
-    const char* v = getenv("AST_MB_ED5");
-    return v ? atoi(v) : 2;
-  }();
-  if (ver == 1) {
-    switch (a.cin_pad / 16) {
-      case 1: return launch_ks5<1>(a, st);
-      case 2: return launch_ks5<2>(a, st);
-      case 3: return launch_ks5<3>(a, st);
-      default: return AST_E_UNSUPPORTED;
-    }
-  }
   switch (a.cin_pad / 16) {
-    case 1: return launch_ks6<1>(a, st);
-    case 2: return launch_ks6<2>(a, st);
-    case 3: return launch_ks6<3>(a, st);
+    case 1: return launch_ks5<1>(a, st);
+    case 2: return launch_ks5<2>(a, st);
+    case 3: return launch_ks5<3>(a, st);
     default: return AST_E_UNSUPPORTED;
   }
 }
