@@ -1073,14 +1073,18 @@ __global__ __launch_bounds__(kThreads) void se_fold_kernel(const float* __restri
   const int n = blockIdx.x;
   for (int c = threadIdx.x; c < hid; c += kThreads) mean[c] = pool[(int64_t)n * hid + c] / hw;
   __syncthreads();
+  // FC1 / FC2: one thread per output, the sum in channel order; unrolled so that 8 weight loads are in
+  // flight at a time (a load-use chain per channel left each launch ~50 us of L2 latency)
   for (int j = threadIdx.x; j < red; j += kThreads) {
     float s = fc1b[j];
+#pragma unroll 8
     for (int c = 0; c < hid; ++c) s = fmaf(fc1w[(int64_t)j * hid + c], mean[c], s);
     hmid[j] = fmaxf(s, 0.f);
   }
   __syncthreads();
   for (int c = threadIdx.x; c < hid; c += kThreads) {
     float s = fc2b[c];
+#pragma unroll 8
     for (int j = 0; j < red; ++j) s = fmaf(fc2w[(int64_t)c * red + j], hmid[j], s);
     gate[c] = fminf(fmaxf(s, 0.f), 1.f);
   }
