@@ -62,6 +62,7 @@ BLOCKS = [
     (40, 24, 1, 6, 5, True, True, (1, 33, 100), 1),    # hidden 240: a half-filled last 32-channel chunk
     (24, 24, 1, 6, 5, False, True, (1, 5, 8), 1),      # map smaller than one tile (reflect on 5 rows)
     (16, 16, 1, 4, 5, True, True, (2, 32, 28), 1),     # exactly one tile, one K-step
+    (20, 16, 1, 3, 5, False, True, (1, 40, 44), 1),    # hidden 60 (past hid16 = 64 in the last chunk), 2 K-steps
 ]
 
 
