@@ -24,6 +24,7 @@
 #include <stdint.h>
 #include "../../include/ast_hip.h"
 #include "x3.h"
+#include "cin3.h"
 
 namespace {
 
@@ -1939,6 +1940,18 @@ int launch_cin4(const ConvArgs& a0, hipStream_t s, int up) {
   return (int)hipGetLastError();
 }
 
+// split-bf16 MFMA conv of a 1..3-channel input (conv_cin3.hip): no pool / upsample
+template <int TH>
+int launch_cin3x3(const ConvArgs& a, hipStream_t s, int up) {
+  if (a.Cin > 3 || a.y_pool || up != 1) return AST_E_UNSUPPORTED;
+  Cin3Args c{};
+  c.x = a.x; c.x2 = a.x2; c.nsplit = a.nsplit; c.wp = a.wp; c.bias = a.bias;
+  c.y_pre = a.y_pre; c.y_act = a.y_act; c.in_mean = a.in_mean; c.in_std = a.in_std;
+  c.e_mask = a.e_mask; c.e_add_pre = a.e_add_pre; c.e_add_post = a.e_add_post;
+  c.N = a.N; c.Cin = a.Cin; c.H = a.H; c.W = a.W; c.Cout = a.Cout; c.cout_pad = a.cout_pad; c.reflect = a.reflect;
+  return launch_conv_cin3_x3(c, TH, s);
+}
+
 int cu_count() {  // CUs of the current device (looked up on a device's first call)
   static int cus_of[64] = {};
   int dev = 0;
@@ -2083,6 +2096,9 @@ const CfgEntry kConfigs[] = {
     {launch_x3<4, 2, 2, 1, true, true>, 64, 8, 2, 0},   // 39: as 29
     {launch_x3<4, 2, 1, 2, true, true>, 32, 8, 2, 0},   // 40: as 30
     {launch_x3<8, 2, 1, 1, true, true>, 32, 16, 2, 0},  // 41: as 31
+    // split-bf16 MFMA conv of a 1..3-channel input, K = 27 in one K-32 block (round 6, conv_cin3.hip)
+    {launch_cin3x3<16>, 64, 16, 1, 0},                  // 42: 16x64 px x 64 ch, 4 waves
+    {launch_cin3x3<8>, 64, 8, 1, 0},                    // 43: 8x64 px x 64 ch, 4 waves
 };
 constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -2092,7 +2108,10 @@ int auto_config(int cin, int cout, int n, int h, int w, int up, bool pool, bool 
   if (cout <= 4 && up == 1 && !pool && !norm && (w & 3) == 0) return cout <= 3 ? 36 : 37;
   if (cout <= 3) return 10;
   if (cout <= 4) return 11;
-  if (cin <= 4 && up == 1 && !pool) return 20;  // direct conv: image-input convs (conv_1)
+  // image-input convs (conv_1) and the decoder's last input gradient: the split-bf16 MFMA kernel for
+  // cin <= 3 (profiles/r06c3_ab5.txt: 16 x 64 x 512^2 conv_1 0.41 -> 0.31 ms), else the direct conv
+  if (cin <= 3 && up == 1 && !pool) return 42;
+  if (cin <= 4 && up == 1 && !pool) return 20;
   if (cin >= kX3K && !norm && (long)cin * (h / up) * (w / up) * 4 < (1L << 31)) {
     // split-bf16 MFMA (fp32-accurate, 2.67x the fp32 matrix rate): 8x32 px x 32 ch tiles, two
     // workgroups per CU; upsampled convs the 16-row tile (profiles/r02_conv_cfgs.log)
@@ -2214,8 +2233,11 @@ int ast_conv3x3_dgrad_f32(int cfg, const float* dy, const float* w_tf_packed, fl
   if ((int64_t)round_up(cout, kCinAlign) * 9 * round_up(cin, kCoutAlign) >= ((int64_t)1 << 31)) return AST_E_SHAPE;
   const bool sum2 = upsample == 2;
   if (cfg < 0) cfg = auto_config(cout, cin, n, h, w, 1, sum2, false);
-  // the epilogue is in the split-bf16 kernels (24-35) and, without the 2x2 sum, the cin <= 4 kernels (18-23)
-  if (!((cfg >= 24 && cfg <= 35) || (cfg >= 18 && cfg <= 23 && !sum2)) || cfg >= kNumConfigs) return AST_E_UNSUPPORTED;
+  // the epilogue is in the split-bf16 kernels (24-35) and, without the 2x2 sum, the cin <= 4 kernels
+  // (18-23) and the cin <= 3 MFMA kernels (42, 43)
+  if (!((cfg >= 24 && cfg <= 35) || (((cfg >= 18 && cfg <= 23) || cfg == 42 || cfg == 43) && !sum2)) ||
+      cfg >= kNumConfigs)
+    return AST_E_UNSUPPORTED;
   static const int m16 = [] {
     const char* v = getenv("AST_CONV_M16");
     return v ? atoi(v) : 1;

@@ -170,7 +170,8 @@ int ast_pad_up_adjoint_f32(const float* dp_full, float* dx, long long planes, in
  * add_post [n, cin, h/up, w/up], each optional: no mask keeps every element, no add_post reads 0).
  * Reflect padding's border fold is ast_dgrad_reflect_border_f32, run after this.
  * The epilogue is the split-bf16 kernels' (cfg 24-35) and, for upsample 1, the cout <= 4 direct
- * kernels' (cfg 18-23; -1 = heuristic): AST_E_UNSUPPORTED for any other configuration -- the
+ * kernels' (cfg 18-23) and the cout <= 3 split-bf16 ones' (cfg 42, 43; -1 = heuristic):
+ * AST_E_UNSUPPORTED for any other configuration -- the
  * caller then runs ast_conv3x3_fwd_f32_cfg + ast_dgrad_finish_f32. */
 int ast_conv3x3_dgrad_f32(int cfg, const float* dy, const float* w_tf_packed, float* dx,
                           const float* mask, const float* add_pre, const float* add_post, int n,

@@ -174,6 +174,8 @@ def tune_dgrad(mode, table, ncfg):
     report = []
     for shp in dgrad_shapes(mode):
         n, cout, H, W, cin, up, hm, hp, hq = shp
+        if os.environ.get("TUNE_CIN3") and cout > 3:  # the input-gradient conv's input is dy (cout channels)
+            continue
         h, w = H // up, W // up
         dy = torch.from_numpy(synth.image(7, (n, cout, H, W))).to(dev)
         wt = torch.from_numpy(synth.conv_weight(8, cout, cin, 3)).to(dev)
@@ -182,7 +184,7 @@ def tune_dgrad(mode, table, ncfg):
         side = lambda on, seed: torch.from_numpy(synth.image(seed, (n, cin, h, w))).to(dev) if on else None  # noqa: E731
         mask, ap, aq = side(hm, 9), side(hp, 10), side(hq, 11)
         res = {}
-        for cfg in range(ncfg):
+        for cfg in cfg_list(ncfg):
             t = time_dgrad(cfg, dy, packed, dx, mask, ap, aq, shp)
             if t is not None:
                 res[cfg] = t
@@ -197,6 +199,12 @@ def tune_dgrad(mode, table, ncfg):
         report.append(row)
         print(json.dumps(row), flush=True)
     return report
+
+
+def cfg_list(ncfg):
+    """TUNE_CFGS=a,b,...: time only these configurations (the others keep losing on these shapes)."""
+    v = os.environ.get("TUNE_CFGS")
+    return [int(c) for c in v.split(",") if int(c) < ncfg] if v else list(range(ncfg))
 
 
 def time_cfg(cfg, x, wp, b, cout, up, pad, pool):
@@ -239,6 +247,8 @@ def main():
             todo = [t for t in todo if key(*t) not in table]
         if os.environ.get("TUNE_SMALL"):  # only the shapes the direct VALU kernels serve (cin or cout <= 4)
             todo = [t for t in todo if t[1] <= 4 or t[4] <= 4]
+        if os.environ.get("TUNE_CIN3"):  # only the shapes of the cin <= 3 kernels (configurations 42, 43)
+            todo = [t for t in todo if t[1] <= 3]
     for shp in todo:
         n, cin, h, w, cout, up, pad, pool = shp
         x = torch.from_numpy(synth.image(5, (n, cin, h, w))).to(dev)
@@ -247,7 +257,7 @@ def main():
         b = torch.zeros(cout, device=dev)
         flops = 2 * n * h * up * w * up * cout * cin * 9
         res = {}
-        for cfg in range(ncfg):
+        for cfg in cfg_list(ncfg):
             t = time_cfg(cfg, x, wp, b, cout, up, pad, pool)
             if t is not None:
                 res[cfg] = t

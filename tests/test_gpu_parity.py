@@ -319,9 +319,10 @@ def test_one_style_many_contents_stats(hip_device):
 
 @pytest.mark.parametrize("cin,pad,norm", [(3, "zeros", True), (3, "reflect", False), (4, "zeros", False)])
 def test_conv3x3_direct_cin4_matches_mfma(cin, pad, norm, hip_device):
-    """The direct cin <= 4 kernel (cfg 20) accumulates in the MFMA kernel's order (tap-major,
-    channel-minor fmaf chain), so conv_1 gives the same bits either way: swapping kernels cannot
-    move a ReLU / max-pool decision downstream (the training-step gradient test depends on it)."""
+    """The direct cin <= 4 kernel (cfg 20) accumulates in the fp32 MFMA kernel's order (tap-major,
+    channel-minor fmaf chain), so the two give the same bits. (Since round 6 conv_1 runs the
+    split-bf16 cfg 42 by default; the ReLU / max-pool routing the training-step oracle tests use is
+    read from the GPU forward itself, so it follows whichever kernel runs.)"""
     x = torch.from_numpy(synth.image(31 + cin, (2, cin, 24, 160))).to(hip_device)
     wt = torch.from_numpy(synth.conv_weight(32, 64, cin, 3)).to(hip_device)
     b = torch.from_numpy(synth.conv_bias(33, 64)).to(hip_device)
@@ -334,6 +335,79 @@ def test_conv3x3_direct_cin4_matches_mfma(cin, pad, norm, hip_device):
     torch.cuda.synchronize()
     assert torch.equal(p20, p7), float((p20 - p7).abs().max())
     assert torch.equal(a20, a7)
+
+
+CIN3_CASES = [
+    # n, cin, h, w, cout, pad, norm, n2 (second batch of the pair input)
+    (2, 3, 37, 150, 64, "zeros", True, 1),    # conv_1: ragged 16-row and 64-column tiles, content|style pair
+    (1, 3, 16, 64, 40, "reflect", False, 0),  # cout 40: a partial 16-channel block of the second half
+    (1, 2, 9, 70, 130, "zeros", False, 0),    # cin 2, three 64-channel groups, W % 4 != 0
+    (3, 1, 5, 3, 16, "reflect", False, 0),    # cin 1, plane narrower than a 32-pixel block
+]
+
+
+@pytest.mark.parametrize("case", CIN3_CASES)
+def test_conv3x3_cin3_split_bf16(case, hip_device):
+    """The split-bf16 MFMA kernel for cin <= 3 (configurations 42, 43; csrc/conv_cin3.hip) against
+    the float64 oracle at the fp32 bar, on ragged tiles, partial channel blocks and the pair input;
+    its two tile heights are the same arithmetic per output, so they agree bit for bit."""
+    n, cin, h, w, cout, pad, norm, n2 = case
+    x = torch.from_numpy(synth.image(61 + cin, (n + n2, cin, h, w)) * 2 - 0.5)
+    wt = torch.from_numpy(synth.conv_weight(62, cout, cin, 3))
+    bs = torch.from_numpy(synth.conv_bias(63, cout))
+    pre_r, act_r, _ = oracle_conv(x, wt, bs, 1, pad, norm, True)
+    xd, wp, bd = x.to(hip_device), ops.pack_conv3x3(wt.to(hip_device)), bs.to(hip_device)
+    mean = torch.tensor(R.IMNET_MEAN, device=hip_device)[:cin] if norm else None
+    std = torch.tensor(R.IMNET_STD, device=hip_device)[:cin] if norm else None
+    outs = []
+    for cfg in (42, 43):
+        pre, act, _ = ops.conv3x3(xd[:n], wp, bd, cout, pad_mode=pad, in_mean=mean, in_std=std, want_pre=True,
+                                  want_act=True, cfg=cfg, x2=xd[n:] if n2 else None)
+        torch.cuda.synchronize()
+        assert rel_inf(pre, pre_r) <= OP_TOL, (cfg, rel_inf(pre, pre_r))
+        assert rel_inf(act, act_r) <= OP_TOL, cfg
+        outs.append((pre, act))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("parts", ["mask", "all", "none"])
+def test_conv3x3_cin3_dgrad_epilogue(parts, hip_device):
+    """Input gradient of a 64 -> 3 conv (the decoder's last layer) through configurations 42 / 43:
+    the dgrad conv reads the 3 channels of dy; fused ReLU-mask / tap-gradient epilogue against CPU
+    autograd; the configurations agree bit for bit with each other."""
+    from arbitrarystyletransfer_amd._lib import lib as L, ptr, stream_ptr
+    from arbitrarystyletransfer_amd.functional import _TF
+    n, cin, H, W = 2, 64, 19, 100
+    wt = torch.from_numpy(synth.conv_weight(71, 3, cin, 3))
+    dy = torch.from_numpy(synth.image(72, (n, 3, H, W)) * 2 - 1)
+    mask = torch.from_numpy(synth.image(73, (n, cin, H, W)) * 2 - 1).clamp_min(0.0)
+    ap = torch.from_numpy(synth.image(74, (n, cin, H, W)) * 2 - 1)
+    aq = torch.from_numpy(synth.image(75, (n, cin, H, W)) * 2 - 1)
+    xr = torch.zeros((n, cin, H, W), requires_grad=True)
+    (F.conv2d(F.pad(xr, (1, 1, 1, 1)), wt) * dy).sum().backward()
+    g = xr.grad
+    if parts == "none":
+        mask = ap = aq = None
+        ref = g
+    elif parts == "mask":
+        ap = aq = None
+        ref = torch.where(mask > 0, g, torch.zeros_like(g))
+    else:
+        ref = torch.where(mask > 0, aq + (g + ap), aq)
+    d = hip_device
+    to = lambda t: None if t is None else t.to(d)  # noqa: E731
+    dyd, md, apd, aqd = to(dy), to(mask), to(ap), to(aq)
+    wtf = _TF.get(wt.to(d))
+    outs = []
+    for cfg in (42, 43):
+        dx = torch.empty((n, cin, H, W), device=d)
+        rc = L().ast_conv3x3_dgrad_f32(cfg, ptr(dyd), ptr(wtf), ptr(dx), ptr(md), ptr(apd), ptr(aqd), n, 3, H, W,
+                                       cin, 1, stream_ptr(d))
+        assert rc == 0, (cfg, rc)
+        torch.cuda.synchronize()
+        assert rel_inf(dx, ref) <= OP_TOL * 2.5, (cfg, rel_inf(dx, ref))
+        outs.append(dx)
+    assert torch.equal(outs[0], outs[1])
 
 
 def test_torch_ops_equal_ctypes_path(hip_device):
