@@ -20,6 +20,7 @@
 #include <stdlib.h>
 #include "../../include/ast_hip.h"
 #include "x3.h"
+#include "wgco3.h"
 #include "det.h"
 
 namespace {
@@ -1252,16 +1253,25 @@ namespace {
 // tile grid and the number of pixel-range splits (each split's partial dW/db is one workspace slot).
 struct WgPlan {
   bool small;  // wgrad_smallco_kernel
+  bool co3;    // wgrad_co3_kernel (split-bf16 MFMA, Cout <= 3; wgrad_co3.hip)
   int tiles_x, tiles_y, groups;
   int64_t ntiles, tiles_per_block, splits;
 };
 
-WgPlan wgrad_plan(int n, int cin, int h_in, int w_in, int cout, int upsample) {
+int g_wgrad_co3 = 1;  // AST_WGRAD_CO3=0: Cout <= 3 on the VALU kernel (A/B measurements)
+
+WgPlan wgrad_plan(int n, int cin, int h_in, int w_in, int cout, int upsample, bool allow_co3 = true) {
   WgPlan p{};
   const int H = h_in * upsample, W = w_in * upsample;
-  p.small = (cout <= 4 || (cout <= 16 && cin <= 16)) && !g_wgrad_v1;
+  p.co3 = allow_co3 && g_wgrad_co3 && !g_wgrad_v1 && wgrad_co3_supported(cin, h_in, w_in, cout, upsample);
+  p.small = !p.co3 && (cout <= 4 || (cout <= 16 && cin <= 16)) && !g_wgrad_v1;
   int64_t target;
-  if (p.small) {  // VALU reduction (wgrad_smallco_kernel)
+  if (p.co3) {  // q tiles: the padded rows x the interior columns; 64 input channels per workgroup
+    p.tiles_x = cdiv(W, WGCO3_TQW);
+    p.tiles_y = cdiv(H + 2, WGCO3_TQH);
+    p.groups = cdiv(cin, 64);
+    target = 1024;
+  } else if (p.small) {  // VALU reduction (wgrad_smallco_kernel)
     const int cg = cout <= 4 ? 4 : 1;  // input channels per workgroup (accumulators: cout x cg x 9)
     p.tiles_x = cdiv(W, SC_TW);
     p.tiles_y = cdiv(H, SC_TH);
@@ -1286,7 +1296,15 @@ void wgrad_env() {
     return v ? atoi(v) : 0;
   }();
   g_wgrad_v1 = v1;
+  static const int co3 = [] {
+    const char* v = getenv("AST_WGRAD_CO3");
+    return v ? atoi(v) : 1;
+  }();
+  g_wgrad_co3 = co3;
 }
+
+// partial slots a plan needs: its splits, plus the border-column slots of the Cout <= 3 MFMA form
+int64_t wgrad_slots(const WgPlan& p) { return p.splits + (p.co3 ? WGCO3_BORDER_SLOTS : 0); }
 }  // namespace
 
 extern "C" {
@@ -1295,7 +1313,10 @@ long long ast_conv3x3_wgrad_workspace_floats(int n, int cin, int h_in, int w_in,
   if (n <= 0 || cin <= 0 || h_in <= 0 || w_in <= 0 || cout <= 0 || (upsample != 1 && upsample != 2)) return 0;
   wgrad_env();
   const WgPlan p = wgrad_plan(n, cin, h_in, w_in, cout, upsample);
-  return (long long)(p.splits * ((int64_t)cout * cin * 9 + cout));
+  int64_t slots = wgrad_slots(p);
+  if (p.co3)  // an unaligned x falls back to the VALU plan (ast_conv3x3_wgrad_ex_f32)
+    slots = std::max<int64_t>(slots, wgrad_slots(wgrad_plan(n, cin, h_in, w_in, cout, upsample, false)));
+  return (long long)(slots * ((int64_t)cout * cin * 9 + cout));
 }
 
 int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* db, int n, int cin, int h_in,
@@ -1316,8 +1337,27 @@ int ast_conv3x3_wgrad_ex_f32(const float* x, const float* dy, float* dw, float* 
   if (workspace_floats < ast_conv3x3_wgrad_workspace_floats(n, cin, h_in, w_in, cout, upsample)) return AST_E_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   wgrad_env();
-  const WgPlan p = wgrad_plan(n, cin, h_in, w_in, cout, upsample);
+  // the MFMA form's 16-byte row loads need a 16-byte aligned x
+  const WgPlan p = wgrad_plan(n, cin, h_in, w_in, cout, upsample, ((uintptr_t)x & 15) == 0);
   const int64_t wcount = (int64_t)cout * cin * 9;
+  if (p.co3) {
+    WgCo3Args c{};
+    c.x = x; c.dy = dy;
+    const int64_t nslot = wgrad_slots(p);
+    c.dw = workspace;                                     // [slots][cout][cin][9]
+    c.db = db ? workspace + nslot * wcount : nullptr;     // [slots][cout]
+    c.N = n; c.Cin = cin; c.Hin = h_in; c.Win = w_in; c.Cout = cout; c.reflect = pad_mode; c.up = upsample;
+    c.dy_pitch = dy_pitch; c.dy_plane = dy_plane; c.dy_off = dy_offset;
+    c.tiles_x = p.tiles_x; c.tiles_y = p.tiles_y; c.cgroups = p.groups;
+    c.ntiles = p.ntiles; c.tiles_per_block = p.tiles_per_block; c.splits = p.splits;
+    int e = launch_wgrad_co3(c, s);
+    if (e) return e;
+    // the slots summed in slot order (the border-column slots last, present with reflect padding)
+    const int64_t slots = pad_mode ? nslot : p.splits;
+    hipError_t he = ast_det::reduce_cols(workspace, slots, wcount, wcount, 1, 0, dw, 0, false, s);
+    if (he == hipSuccess && db) he = ast_det::reduce_cols(c.db, slots, cout, cout, 1, 0, db, 0, false, s);
+    return (int)he;
+  }
   WgArgs a{};
   a.x = x; a.dy = dy;
   a.dw = workspace;                                      // [splits][cout][cin][9]

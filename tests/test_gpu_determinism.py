@@ -63,6 +63,13 @@ WGRAD_CASES = [
     (2, 24, 13, 9, 40, 1, "zeros"),
     (2, 64, 24, 40, 3, 1, "reflect"),
     (2, 16, 20, 20, 16, 1, "reflect"),
+    # cout <= 3 on the split-bf16 MFMA form (wgrad_co3.hip: W % 16 == 0): ragged 64-column q tiles,
+    # upsample, zero padding (no border slot), few / many input channels
+    (2, 64, 24, 48, 3, 1, "reflect"),
+    (1, 40, 18, 32, 3, 2, "reflect"),
+    (2, 64, 10, 16, 2, 1, "zeros"),
+    (1, 16, 20, 160, 3, 1, "reflect"),
+    (1, 130, 9, 32, 1, 1, "reflect"),
 ]
 
 
