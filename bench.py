@@ -357,9 +357,9 @@ def mobilenet_bench(args, dev, rank, world):
     step_pmc = (None, None)
     if (B, S) == (32, 1024) and not args.attention:
         try:
-            with open(os.path.join(ROOT, "profiles", "r06y_mb_step_traffic.json")) as f:
+            with open(os.path.join(ROOT, "profiles", "r06d_mb_step_traffic.json")) as f:
                 d = json.load(f)
-            step_pmc = (d["hbm_gb_per_step"], "profiles/r06y_mb_step_traffic.json (" + d["source"] + ")")
+            step_pmc = (d["hbm_gb_per_step"], "profiles/r06d_mb_step_traffic.json (" + d["source"] + ")")
         except (OSError, ValueError, KeyError):
             pass
     ed = fam.get("mb expand_dw")
@@ -712,8 +712,8 @@ def main():
                                f"bs={B}/GPU {S}x{S} fp32 forward",
                    "global_batch": B * world, "image_size": S, "parallelism": f"batch-sharded x{world}"},
         "roofline": {"bound": "mfma",
-                     "kernel": "conv3x3 launches of a step (16 split-bf16 MFMA implicit-GEMM + direct VALU conv_1 "
-                               "and 64->3 image conv)",
+                     "kernel": "conv3x3 launches of a step (16 split-bf16 MFMA implicit-GEMM, the split-bf16 "
+                               "cin <= 3 conv_1 and the direct VALU 64->3 image conv)",
                      "achieved": achieved_tf, "peak": PEAK_SPLIT_BF16_TF, "unit": "TFLOP/s",
                      "peak_basis": "fp32-accurate FLOP/s ceiling of the split-bf16 kernel = dense bf16 MFMA "
                                    "2516.6 TF / 6 bf16 products per fp32 product; achieved = algorithmic fp32 "
