@@ -62,7 +62,11 @@ __global__ __launch_bounds__(NT, 2) void wgrad_co3_kernel(WgCo3Args a) {
   const int64_t split = blockIdx.x / a.cgroups;
   const int ci0 = cgi * 64;
   const int64_t t0 = split * a.tiles_per_block, t1 = min(a.ntiles, t0 + a.tiles_per_block);
-  for (int e = tid; e < 2 * 3 * DC; e += NT) Ds[e / (3 * DC)][(e / DC) % 3][ZROW * DC + e % DC] = 0;
+  for (int c = tid; c < DC; c += NT)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) Ds[b][t][ZROW * DC + c] = 0;
 
   // the lane's N column: (co, ky, kx) = n / 9, n % 9 / 3, n % 3; its B row for this wave's q row is
   // r = w - ky + 2 of copy (co, kx)
