@@ -52,7 +52,7 @@ DGRAD_CASES = [
     (2, 32, 18, 70, 48, 2, "reflect"),    # ragged tiles
     (1, 16, 4, 4, 32, 2, "reflect"),      # smallest upsampled map (2x2 source)
     (2, 64, 2, 6, 16, 1, "reflect"),      # 2-row map: both border rows are interior rows 1 and 0
-    (1, 3, 16, 40, 64, 1, "reflect"),     # cout 3: the dgrad conv reads 3 channels -> cin<=4 direct kernel, fused epilogue
+    (1, 3, 16, 40, 64, 1, "reflect"),     # cout 3: the dgrad conv reads 3 channels -> the cin<=3 split-bf16 kernel (cfg 42), fused epilogue
     (4, 64, 16, 40, 64, 1, "zeros"),      # small planes packed side by side -> elementwise epilogue
 ]
 
