@@ -1091,6 +1091,50 @@ __global__ __launch_bounds__(WM * 64, OCC) void conv3x3_x3_kernel(ConvArgs a) {
     __syncthreads();  // every wave is done reading the last chunk's tiles
     X3_ST(2 + 4 * nch);
     float* region = reinterpret_cast<float*>(x3_smem) + wm * 32 * RM * 36;
+    // ReLU + 2x2 max-pool as the only output (the encoder's pool layers in config 2): pooled in
+    // registers -- a lane holds both rows of its windows (acc16[2pr], acc16[2pr + 1]) and 4
+    // consecutive pixels -- with no LDS round trip. One exchange with lane ^ 16 gives every lane 4
+    // consecutive pooled pixels: even g16 its own pair and the partner's of tile pt = 0, odd g16 the
+    // partner's and its own of pt = 1, so the 4 lanes of a channel store its 16 pooled pixels as one
+    // 64-byte run (store_region's granularity). Same max_nan order as store_region: bit-identical.
+    if (a.y_pool && !a.y_pre && !a.y_act && !a.e_sum2 && !dgrad_epi(a)) {
+      const int Ho = a.H >> 1, Wo = a.W >> 1;
+      const bool odd = g16 & 1;
+      const int pc = (x0 >> 1) + (odd ? 8 + 2 * (g16 - 1) : 2 * g16);
+      const bool vec = (Wo & 3) == 0 && pc + 3 < Wo;
+#pragma unroll
+      for (int q = 0; q < 2 * RN; ++q) {
+        const int co = n0 + 16 * q + l16;
+        const float bv = (co < a.Cout && a.bias) ? a.bias[co] : 0.f;
+#pragma unroll
+        for (int pr = 0; pr < RM / 2; ++pr) {
+          float pv[2][2];
+#pragma unroll
+          for (int pt = 0; pt < 2; ++pt) {
+            const f32x4v r0 = acc16[2 * pr][pt][q], r1 = acc16[2 * pr + 1][pt][q];
+            const float m0 = max_nan(relu_f(r0[0] + bv), relu_f(r1[0] + bv));
+            const float m1 = max_nan(relu_f(r0[1] + bv), relu_f(r1[1] + bv));
+            const float m2 = max_nan(relu_f(r0[2] + bv), relu_f(r1[2] + bv));
+            const float m3 = max_nan(relu_f(r0[3] + bv), relu_f(r1[3] + bv));
+            pv[pt][0] = max_nan(m0, m1);
+            pv[pt][1] = max_nan(m2, m3);
+          }
+          const float e0 = __shfl_xor(odd ? pv[0][0] : pv[1][0], 16, 64);
+          const float e1 = __shfl_xor(odd ? pv[0][1] : pv[1][1], 16, 64);
+          const float o[4] = {odd ? e0 : pv[0][0], odd ? e1 : pv[0][1], odd ? pv[1][0] : e0, odd ? pv[1][1] : e1};
+          const int py = ((y0 + wm * RM) >> 1) + pr;
+          if (co >= a.Cout || py >= Ho) continue;
+          float* dst = a.y_pool + ((int64_t)n * a.Cout + co) * Ho * Wo + (int64_t)py * Wo + pc;
+          if (vec) {
+            *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (pc + k < Wo) dst[k] = o[k];
+          }
+        }
+      }
+    } else
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
 #pragma unroll

@@ -131,6 +131,40 @@ def test_conv3x3_persistent_bit_identical(case, hip_device):
                     assert torch.equal(r, g), (pc, (r - g).abs().max().item())
 
 
+POOL_ONLY_CASES = [
+    # n, cin, h, w, cout, pad: the encoder's pool layers, ragged tiles, W/2 % 4 != 0, partial channel tiles
+    (2, 64, 32, 64, 64, "zeros"),
+    (1, 40, 18, 70, 48, "zeros"),
+    (3, 128, 17, 36, 128, "reflect"),
+    (1, 16, 6, 10, 24, "zeros"),
+]
+
+
+@pytest.mark.parametrize("case", POOL_ONLY_CASES)
+def test_conv3x3_pool_only_bit_identical(case, hip_device):
+    """ReLU + max-pool as the only output (config 2's encoder pool layers): the split-bf16 M16 kernels
+    pool in registers (no LDS staging); the pooled map must equal, bit for bit, the pool the same
+    configuration writes beside the pre-ReLU and ReLU maps (the staged path), and the oracle."""
+    n, cin, h, w, cout, pad = case
+    x = torch.from_numpy(synth.image(81 + cin, (n, cin, h, w)) * 2 - 0.5)
+    wt = torch.from_numpy(synth.conv_weight(82, cout, cin, 3))
+    bs = torch.from_numpy(synth.conv_bias(83, cout))
+    _, _, pool_r = oracle_conv(x, wt, bs, 1, pad, False, True)
+    xd, wp, bd = x.to(hip_device), ops.pack_conv3x3(wt.to(hip_device)), bs.to(hip_device)
+    for cfg in (-1, 28, 29, 30, 31, 38, 39, 40, 41):
+        try:
+            _, _, p_only = ops.conv3x3(xd, wp, bd, cout, pad_mode=pad, want_pre=False, want_act=False,
+                                       want_pool=True, cfg=cfg)
+            _, _, p_all = ops.conv3x3(xd, wp, bd, cout, pad_mode=pad, want_pre=True, want_act=True, want_pool=True,
+                                      cfg=cfg)
+        except Exception as e:
+            assert "unsupported" in str(e), e
+            continue
+        torch.cuda.synchronize()
+        assert torch.equal(p_only, p_all), (cfg, float((p_only - p_all).abs().max()))
+        assert rel_inf(p_only, pool_r) <= OP_TOL, (cfg, rel_inf(p_only, pool_r))
+
+
 @pytest.mark.parametrize("cin", [1, 2, 3, 4])
 def test_conv3x3_direct_cin_le4_lds_weights(cin, hip_device):
     """The direct cin <= 4 kernel (configs 18-23) on every cin it takes, with a 192-channel weight
