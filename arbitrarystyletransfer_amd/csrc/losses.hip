@@ -12,8 +12,10 @@
 //  * Huber: delta = 1, reduction 'mean' (F.huber_loss default).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "../../include/ast_hip.h"
 #include "det.h"
+#include "x3.h"
 
 namespace {
 
@@ -638,6 +640,137 @@ __global__ __launch_bounds__(256) void gram_kernel(const float* __restrict__ F, 
   }
 }
 
+// Gram forward on the split-bf16 matrix cores (round 6; AST_GRAM_X3=0 selects gram_kernel above).
+// Every gram of the style loss is 2 C^2 HW B = 34 GFLOP (C^2 HW is the same at every VGG tap); the
+// LDS-staged gram_kernel runs them at 91-147 TF on the fp32 MFMA, bound by its per-chunk staging
+// and barriers rather than by the MFMA (an LDS-staged split-bf16 form of it was no faster). Here
+// there is no LDS and no barrier in the K loop: the 4 waves of a
+// workgroup take interleaved 16-k steps of the workgroup's K range, and each computes the whole
+// 64 x 64 tile (2 x 2 blocks of v_mfma_f32_32x32x16_bf16, the six term products). A lane loads its
+// 8 consecutive k of 2 (diagonal tile) or 4 rows straight from HBM, one step ahead, and splits them
+// in registers (ast_x3::split8). The 4 partial tiles meet in LDS at the end, summed in wave order.
+// B = 8: 189 / 202 / 163 / 155 -> 145 / 141 / 140 / 124 us at C = 64 / 128 / 256 / 512
+// (profiles/r06gx_gram_ab.txt).
+__global__ __launch_bounds__(256, 2) void gram_x3_kernel(const float* __restrict__ F, float* __restrict__ G, int C,
+                                                         int64_t K, int64_t kchunk, float s) {
+  typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+  __shared__ float red[3][64][65];  // waves 1..3's tiles for wave 0 to add
+  const int tiles = (C + GT - 1) / GT;
+  int ti = 0, tj = blockIdx.x;  // upper-triangle index -> (ti, tj), ti <= tj
+  while (tj >= tiles - ti) {
+    tj -= tiles - ti;
+    ++ti;
+  }
+  tj += ti;
+  const int b = blockIdx.z;
+  const int64_t k0 = (int64_t)blockIdx.y * kchunk;
+  const int64_t k1 = min(K, k0 + kchunk);
+  const float* Fb = F + (int64_t)b * C * K;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const bool diag = ti == tj;
+  const bool vec = ((K & 3) == 0) && ((k0 & 3) == 0);
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[u][v][r] = 0.f;
+  // this lane's rows: A rows ti*64 + 32u + l32, B rows tj*64 + 32v + l32 (= A's on a diagonal tile)
+  const float* ra[2];
+  const float* rb[2];
+  bool oka[2], okb[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = ti * GT + 32 * u + l32, j = tj * GT + 32 * u + l32;
+    oka[u] = i < C;
+    okb[u] = j < C;
+    ra[u] = Fb + (int64_t)(oka[u] ? i : 0) * K;
+    rb[u] = Fb + (int64_t)(okb[u] ? j : 0) * K;
+  }
+  float xa[2][8], xb[2][8];
+  auto load = [&](int64_t kk) {  // k = kk + 8h .. +7 of every row
+    const int64_t kq = kk + 8 * h;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (vec && kq + 7 < k1) {
+        const float4 p0 = oka[u] ? *reinterpret_cast<const float4*>(ra[u] + kq) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 p1 = oka[u] ? *reinterpret_cast<const float4*>(ra[u] + kq + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        xa[u][0] = p0.x; xa[u][1] = p0.y; xa[u][2] = p0.z; xa[u][3] = p0.w;
+        xa[u][4] = p1.x; xa[u][5] = p1.y; xa[u][6] = p1.z; xa[u][7] = p1.w;
+        if (!diag) {
+          const float4 q0 = okb[u] ? *reinterpret_cast<const float4*>(rb[u] + kq) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 q1 = okb[u] ? *reinterpret_cast<const float4*>(rb[u] + kq + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+          xb[u][0] = q0.x; xb[u][1] = q0.y; xb[u][2] = q0.z; xb[u][3] = q0.w;
+          xb[u][4] = q1.x; xb[u][5] = q1.y; xb[u][6] = q1.z; xb[u][7] = q1.w;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const bool in = kq + q < k1;
+          xa[u][q] = (in && oka[u]) ? ra[u][kq + q] : 0.f;
+          if (!diag) xb[u][q] = (in && okb[u]) ? rb[u][kq + q] : 0.f;
+        }
+      }
+    }
+  };
+  int64_t kk = k0 + 16 * wave;
+  if (kk < k1) load(kk);
+  for (; kk < k1; kk += 64) {
+    bf16x8_t ta[2][3], tb[2][3];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      ast_x3::split8(xa[u], ta[u][0], ta[u][1], ta[u][2]);
+      if (!diag) ast_x3::split8(xb[u], tb[u][0], tb[u][1], tb[u][2]);
+    }
+    if (kk + 64 < k1) load(kk + 64);  // the wave's next step, in flight during these MFMAs
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        if (diag && u > v) continue;  // the lower-left block of a diagonal tile is the mirror
+        const bf16x8_t* bv = diag ? ta[v] : tb[v];
+        f32x16 c = acc[u][v];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ta[u][2], bv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ta[u][0], bv[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ta[u][1], bv[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ta[u][1], bv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ta[u][0], bv[1], c, 0, 0, 0);
+        acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ta[u][0], bv[0], c, 0, 0, 0);
+      }
+  }
+  // C layout: block (u, v), lane (col l32, half h), element r -> row 32u + (r & 3) + 8 (r >> 2) + 4h,
+  // column 32v + l32 of the tile
+  if (wave > 0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          red[wave - 1][32 * u + (r & 3) + 8 * (r >> 2) + 4 * h][32 * v + l32] = acc[u][v][r];
+  }
+  __syncthreads();
+  if (wave > 0) return;
+  float* Gb = G + ((int64_t)blockIdx.y * gridDim.z + b) * C * C;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      if (diag && u > v) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int li = 32 * u + (r & 3) + 8 * (r >> 2) + 4 * h, lj = 32 * v + l32;
+        const int i = ti * GT + li, j = tj * GT + lj;
+        const float t = ((acc[u][v][r] + red[0][li][lj]) + red[1][li][lj]) + red[2][li][lj];
+        if (i < C && j < C && (ti != tj || i <= j)) {  // diagonal tiles: the upper half, mirrored
+          Gb[(int64_t)i * C + j] = s * t;
+          Gb[(int64_t)j * C + i] = s * t;
+        }
+      }
+    }
+}
+
 // Gram backward: dF[b][i][n] (+)= s * sum_k (dG[k][i] + dG[i][k]) F[b][k][n] + ra[b,i] F[b][i][n] + rb[b,i].
 // Output tile 64 (i) x 128 (n); 4 waves 2x2, each 32 x 64; BK = 16.
 constexpr int BI = 64, BNN = 128, BBK = 16;
@@ -787,8 +920,12 @@ int ast_gram_f32(const float* feat, float* gram, int n, int c, long long hw, flo
     if (!workspace) return AST_E_NULLPTR;
     if (workspace_floats < ast_gram_workspace_floats(n, c, hw)) return AST_E_SHAPE;
   }
-  hipLaunchKernelGGL(gram_kernel, dim3(tiles * (tiles + 1) / 2, (unsigned)splits, n), dim3(256), 0, s, feat,
-                     splits > 1 ? workspace : gram, c, (int64_t)hw, kchunk, scale);
+  static const int x3 = [] {  // AST_GRAM_X3=0: the fp32 MFMA gram_kernel (A/B measurements)
+    const char* v = getenv("AST_GRAM_X3");
+    return v ? atoi(v) : 1;
+  }();
+  hipLaunchKernelGGL(x3 ? gram_x3_kernel : gram_kernel, dim3(tiles * (tiles + 1) / 2, (unsigned)splits, n), dim3(256),
+                     0, s, feat, splits > 1 ? workspace : gram, c, (int64_t)hw, kchunk, scale);
   if (splits > 1) {
     const int64_t cnt = (int64_t)n * c * c;
     const hipError_t e = ast_det::reduce_cols(workspace, splits, cnt, cnt, 1, 0, gram, 0, false, s);

@@ -43,6 +43,11 @@ if __name__ == "__main__":
         rb = torch.empty(planes, device="cuda")
         t_s = timed(lambda: lib().ast_style_moments_ws_f32(ptr(x), ptr(y), planes, hw, 1.0, None, ptr(st), ptr(loss),
                                                            ptr(ra), ptr(rb), ptr(ws), ws.numel(), Fn._s(x)))
+        dx = torch.empty_like(x)
+        Fn.mvn_huber(x, y, 1.0, loss, ps)
+        t_b = timed(lambda: lib().ast_mvn_huber_backward_f32(ptr(x), ptr(y), ptr(ps), planes, hw, 1.0, None, ptr(dx), 0,
+                                                              Fn._s(x)))
+        print(f"  mvn_huber_backward {t_b * 1e3:7.1f} us ({3 * x.numel() * 4 / t_b / 1e6:5.0f} GB/s)", flush=True)
         gx = torch.empty(n, c, c, device="cuda")
         t_g = timed(lambda: Fn.gram(x, gx, 1.0 / (c * hw)))
         print(f"{n}x{c}x{s}^2: mvn_huber {t_m * 1e3:7.1f} us ({2 * nbytes / t_m / 1e6:5.0f} GB/s over 2 passes)   "
