@@ -48,6 +48,13 @@ if __name__ == "__main__":
         t_b = timed(lambda: lib().ast_mvn_huber_backward_f32(ptr(x), ptr(y), ptr(ps), planes, hw, 1.0, None, ptr(dx), 0,
                                                               Fn._s(x)))
         print(f"  mvn_huber_backward {t_b * 1e3:7.1f} us ({3 * x.numel() * 4 / t_b / 1e6:5.0f} GB/s)", flush=True)
+        dG = torch.rand(n, c, c, device="cuda")
+        raa = torch.rand(planes, device="cuda")
+        rbb = torch.rand(planes, device="cuda")
+        t_gb = timed(lambda: lib().ast_gram_backward_f32(ptr(x), ptr(dG), ptr(dx), ptr(raa), ptr(rbb), n, c, hw,
+                                                          1.0 / (c * hw), None, 0, Fn._s(x)))
+        print(f"  gram_backward {t_gb * 1e3:7.1f} us ({2 * c * c * hw * n * 2 / t_gb / 1e9:5.0f} TF, "
+              f"{3 * x.numel() * 4 / t_gb / 1e6:5.0f} GB/s over F read twice + dF)", flush=True)
         gx = torch.empty(n, c, c, device="cuda")
         t_g = timed(lambda: Fn.gram(x, gx, 1.0 / (c * hw)))
         print(f"{n}x{c}x{s}^2: mvn_huber {t_m * 1e3:7.1f} us ({2 * nbytes / t_m / 1e6:5.0f} GB/s over 2 passes)   "
