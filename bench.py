@@ -357,9 +357,9 @@ def mobilenet_bench(args, dev, rank, world):
     step_pmc = (None, None)
     if (B, S) == (32, 1024) and not args.attention:
         try:
-            with open(os.path.join(ROOT, "profiles", "r06d_mb_step_traffic.json")) as f:
+            with open(os.path.join(ROOT, "profiles", "r06k_mb_step_traffic.json")) as f:
                 d = json.load(f)
-            step_pmc = (d["hbm_gb_per_step"], "profiles/r06d_mb_step_traffic.json (" + d["source"] + ")")
+            step_pmc = (d["hbm_gb_per_step"], "profiles/r06k_mb_step_traffic.json (" + d["source"] + ")")
         except (OSError, ValueError, KeyError):
             pass
     ed = fam.get("mb expand_dw")

@@ -5,7 +5,7 @@ import sys
 
 MFMA = ("conv3x3_x3_kernel", "conv3x3_x3p_kernel", "wgrad3_kernel", "wgrad2_kernel", "wgrad_kernel", "gram_kernel",
         "gram_bwd_kernel", "gemm_kernel", "gemm_wide_kernel", "gemm_x3_kernel", "conv3x3_f32_kernel",
-        "conv3x3_cin3_x3_kernel", "wgrad_co3_kernel")  # round 6: the split-bf16 cin <= 3 conv and cout <= 3 wgrad
+        "conv3x3_cin3_x3_kernel", "wgrad_co3_kernel", "gram_x3_kernel")  # round 6: split-bf16 cin <= 3 conv, cout <= 3 wgrad, Gram
 VALU_CONV = ("conv3x3_cin4_kernel", "conv3x3_smallc", "wgrad_smallco_kernel")
 tot = 0.0
 cls = {"mfma": 0.0, "valu conv": 0.0, "other": 0.0}
