@@ -773,7 +773,11 @@ __global__ __launch_bounds__(256, 2) void gram_x3_kernel(const float* __restrict
 
 // Gram backward: dF[b][i][n] (+)= s * sum_k (dG[k][i] + dG[i][k]) F[b][k][n] + ra[b,i] F[b][i][n] + rb[b,i].
 // Output tile 64 (i) x 128 (n); 4 waves 2x2, each 32 x 64; BK = 16.
-constexpr int BI = 64, BNN = 128, BBK = 16;
+#ifndef GRAM_BWD_BK  // K chunk per barrier pair; 32 and 64 were slower (fewer resident workgroups:
+#define GRAM_BWD_BK 16  // profiles/r06gbk_gram_bwd_bk.txt)
+#endif
+constexpr int BI = 64, BNN = 128, BBK = GRAM_BWD_BK;
+constexpr int BS_T = BBK * BI / 256, BF_T = BBK * BNN / 4 / 256;  // S entries / F float4 per thread
 
 __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__ F, const float* __restrict__ dG,
                                                        float* __restrict__ dF, const float* __restrict__ ra,
@@ -794,20 +798,20 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
   // the next k-chunk's S and F values in registers while the current chunk's MFMAs run
-  float sv[4];
-  float4 fv[2];
+  float sv[BS_T];
+  float4 fv[BF_T];
   auto load = [&](int k0) {
-    // S tile: 16 k x 64 i = 1024 entries, 4 per thread
+    // S tile: BBK k x 64 i, BS_T entries per thread
 #pragma unroll
-    for (int rep = 0; rep < 4; ++rep) {
+    for (int rep = 0; rep < BS_T; ++rep) {
       const int e = tid + rep * 256;
       const int kk = e >> 6, ii = e & 63;
       const int k = k0 + kk, i = ti * BI + ii;
       sv[rep] = (k < C && i < C) ? dGb[(int64_t)k * C + i] + dGb[(int64_t)i * C + k] : 0.f;
     }
-    // F tile: 16 k x 128 n = 512 float4 -> 2 per thread
+    // F tile: BBK k x 128 n, BF_T float4 per thread
 #pragma unroll
-    for (int rep = 0; rep < 2; ++rep) {
+    for (int rep = 0; rep < BF_T; ++rep) {
       const int e = tid + rep * 256;
       const int kk = e >> 5, nq = (e & 31) * 4;
       const int k = k0 + kk;
@@ -829,12 +833,12 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
   load(0);
   for (int k0 = 0; k0 < C; k0 += BBK) {
 #pragma unroll
-    for (int rep = 0; rep < 4; ++rep) {
+    for (int rep = 0; rep < BS_T; ++rep) {
       const int e = tid + rep * 256;
       As[e >> 6][e & 63] = sv[rep];
     }
 #pragma unroll
-    for (int rep = 0; rep < 2; ++rep) {
+    for (int rep = 0; rep < BF_T; ++rep) {
       const int e = tid + rep * 256;
       *reinterpret_cast<float4*>(&Bs[e >> 5][(e & 31) * 4]) = fv[rep];
     }
