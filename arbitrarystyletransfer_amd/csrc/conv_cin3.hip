@@ -64,7 +64,7 @@ __device__ __forceinline__ unsigned short bits(bf16 v) { return __builtin_bit_ca
 // bias), its mask loaded before the block's MFMAs; otherwise bias + y_pre / y_act. The epilogue
 // modes are template / wave-uniform branches around whole store loops: a per-element choice between
 // the store-only and the load-using paths made the compiler wait on vmcnt -- which on gfx9 also
-// counts stores -- once per element (0.51 ms for the config-2 conv_1 against 0.23 ms unified).
+// counts stores -- once per element (0.51 ms for the config-2 conv_1 against 0.31 ms unified).
 template <int TH, bool NORM, bool DG>
 __global__ __launch_bounds__(NT, DG ? 2 : 3) void conv3x3_cin3_x3_kernel(Cin3Args a) {
   using C = C3<TH>;
